@@ -1,0 +1,141 @@
+"""ctypes binding of ``libflipchain.so`` (the C-ABI declared in ``include/flipchain.h``).
+
+The library is required: there is no CPU fallback.  Importing this module builds the
+in-tree library if it is missing and the toolchain is present, and raises otherwise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import build as _build
+
+_P = ctypes.POINTER
+
+FC_OK = 0
+FC_ERR_ARG = -1
+FC_ERR_INVALID_STATE = -2
+FC_ERR_HIP = -3
+FC_ERR_UNSUPPORTED = -4
+FC_ERR_NOMEM = -5
+
+FC_GRAPH_NO_EXACT = 0x1
+FC_PROPOSE_BI_SIGN = 0
+FC_DIAG_WAIT, FC_DIAG_HIST, FC_DIAG_EDGES, FC_DIAG_FLIPS = 0x1, 0x2, 0x4, 0x8
+FC_FLAG_FORCE_BFS = 0x1
+
+EXPORTED = [
+    "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
+    "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_sync", "fc_run_last_ms",
+    "fc_run_read_stats", "fc_run_read_state", "fc_run_read_trace", "fc_run_read_hist",
+    "fc_run_read_edges", "fc_run_read_flips", "fc_run_n_chains", "fc_run_destroy",
+    "fc_device_count", "fc_last_error",
+]
+
+
+class GraphInfo(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int32), ("n_edges", ctypes.c_int32), ("ring_max", ctypes.c_int32),
+                ("max_degree", ctypes.c_int32), ("n_exact", ctypes.c_int32), ("n_gamma", ctypes.c_int32),
+                ("planar", ctypes.c_int32), ("outer_simple", ctypes.c_int32)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_int32), ("proposal", ctypes.c_int32), ("base", ctypes.c_double),
+                ("pop_lo", ctypes.c_int64), ("pop_hi", ctypes.c_int64), ("seed", ctypes.c_uint64),
+                ("chain_id_offset", ctypes.c_uint32), ("diag_mask", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("device", ctypes.c_int32), ("trace_chains", ctypes.c_int32),
+                ("trace_cap", ctypes.c_int64), ("labels", _P(ctypes.c_int32)), ("log1mp", _P(ctypes.c_double))]
+
+
+class ChainStats(ctypes.Structure):
+    _fields_ = [("steps", ctypes.c_int64), ("proposals", ctypes.c_int64), ("draws", ctypes.c_int64),
+                ("accepted", ctypes.c_int64), ("inv_contig", ctypes.c_int64), ("inv_pop", ctypes.c_int64),
+                ("sum_cut", ctypes.c_int64), ("sum_nb", ctypes.c_int64), ("sum_wait", ctypes.c_int64),
+                ("sum_cut2", ctypes.c_int64), ("sum_nb2", ctypes.c_int64), ("wait_cur", ctypes.c_int64),
+                ("bfs_calls", ctypes.c_int64), ("bfs_levels", ctypes.c_int64),
+                ("cut", ctypes.c_int32), ("nb", ctypes.c_int32), ("last_flip", ctypes.c_int32),
+                ("stuck", ctypes.c_int32)]
+
+
+class Record(ctypes.Structure):
+    _fields_ = [("draw", ctypes.c_int64), ("v", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("cut", ctypes.c_int32), ("nb", ctypes.c_int32), ("wait", ctypes.c_int64)]
+
+
+class FlipChainError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load(build_if_missing: bool = True):
+    """Load (building if needed) the native library; raises when it cannot be had."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if build_if_missing and (not os.path.exists(path) or _build._stale()):
+        if os.path.exists(_build.HIPCC):
+            _build.build()
+    if not os.path.exists(path):
+        raise ImportError(f"libflipchain.so not found at {path}: run `python -m flipcomplexityempirical_amd.build` "
+                          "(the HIP path is required; there is no CPU fallback)")
+    L = ctypes.CDLL(path)
+    i32, i64, u32, dbl = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_double
+    vp = ctypes.c_void_p
+    L.fc_graph_create.argtypes = [i32, _P(i32), _P(i32), _P(i32), _P(dbl), u32, _P(vp)]
+    L.fc_graph_get_info.argtypes = [vp, _P(GraphInfo)]
+    L.fc_graph_edges.argtypes = [vp, _P(i32), _P(i32)]
+    L.fc_graph_rings.argtypes = [vp, _P(i32), _P(ctypes.c_uint64)]
+    L.fc_graph_destroy.argtypes = [vp]
+    L.fc_graph_destroy.restype = None
+    L.fc_run_create.argtypes = [vp, _P(Params), i32, _P(ctypes.c_int8), _P(dbl), _P(vp)]
+    L.fc_run_steps.argtypes = [vp, i64, i64, vp]
+    L.fc_run_set_tape.argtypes = [vp, _P(ctypes.c_uint32), i64]
+    L.fc_run_sync.argtypes = [vp]
+    L.fc_run_last_ms.argtypes = [vp, _P(ctypes.c_float)]
+    L.fc_run_read_stats.argtypes = [vp, _P(ChainStats)]
+    L.fc_run_read_state.argtypes = [vp, _P(ctypes.c_int8)]
+    L.fc_run_read_trace.argtypes = [vp, i32, _P(Record), i64, _P(i64)]
+    L.fc_run_read_hist.argtypes = [vp, _P(i64), _P(i64)]
+    L.fc_run_read_edges.argtypes = [vp, _P(i64)]
+    L.fc_run_read_flips.argtypes = [vp, _P(i64), _P(i64), _P(i64)]
+    L.fc_run_n_chains.argtypes = [vp]
+    L.fc_run_n_chains.restype = i32
+    L.fc_run_destroy.argtypes = [vp]
+    L.fc_run_destroy.restype = None
+    L.fc_device_count.argtypes = [_P(i32)]
+    L.fc_last_error.argtypes = []
+    L.fc_last_error.restype = ctypes.c_char_p
+    for name in EXPORTED:
+        if name not in ("fc_graph_destroy", "fc_run_destroy", "fc_last_error", "fc_run_n_chains"):
+            getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == FC_OK:
+        return
+    msg = (load().fc_last_error() or b"").decode(errors="replace")
+    text = f"{what}: {msg}" if what else msg
+    if rc == FC_ERR_INVALID_STATE:
+        raise ValueError(text)
+    if rc == FC_ERR_ARG:
+        raise ValueError(text)
+    if rc == FC_ERR_UNSUPPORTED:
+        raise NotImplementedError(text)
+    if rc == FC_ERR_NOMEM:
+        raise MemoryError(text)
+    raise FlipChainError(text)
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    rc = load().fc_device_count(ctypes.byref(n))
+    return int(n.value) if rc == FC_OK else 0

@@ -1,0 +1,46 @@
+"""In-tree build of ``libflipchain.so`` for gfx950 (``hipcc``; no JIT cache, no CMake).
+
+The shared library lands next to this file so that it travels to the GPU box with the
+repository snapshot.  ``python -m flipcomplexityempirical_amd.build`` rebuilds it.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libflipchain.so")
+SOURCES = ["fc_kernels.hip", "fc_capi.cpp", "fc_graph.cpp"]
+HEADERS = ["fc_internal.h", "fc_philox.h", os.path.join("..", "..", "include", "flipchain.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("FC_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-o", LIB]
+    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
+    if verbose and res.stderr:
+        print(res.stderr, file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,561 @@
+// C-ABI of libflipchain.so (include/flipchain.h): graph and run lifetime, initial-state
+// validation and set-up on the host, kernel launches and readouts.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "fc_internal.h"
+#include "fc_philox.h"
+
+struct fc_graph {
+    fc::HostGraph h;
+};
+
+struct fc_run {
+    fc::HostGraph g;  // host copy (sizes, edges, rings for readouts)
+    fc_params p{};
+    std::vector<int32_t> labels;
+    std::vector<double> log1mp;
+    int32_t n_chains = 0;
+    int32_t npad = 0;
+    int32_t words = 0;
+    int32_t chain_lds_bytes = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    // device buffers
+    void *d_graph = nullptr;
+    int32_t *d_ring_eid = nullptr;
+    int8_t *d_assign = nullptr;
+    uint8_t *d_fcnt = nullptr;
+    fc::ChainScalars *d_sc = nullptr;
+    uint64_t *d_thresh = nullptr;
+    double *d_log1mp = nullptr;
+    int32_t *d_labels = nullptr;
+    int64_t *d_cut_hist = nullptr, *d_nb_hist = nullptr;
+    int64_t *d_edge_acc = nullptr, *d_edge_since = nullptr;
+    int64_t *d_num_flips = nullptr, *d_part_sum = nullptr, *d_last_flipped = nullptr;
+    fc_record *d_trace = nullptr;
+    uint32_t *d_tape = nullptr;
+    int64_t tape_draws = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return fail(FC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T>
+int dalloc(T **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return FC_OK;
+    hipError_t e = hipMalloc((void **)p, count * sizeof(T));
+    if (e != hipSuccess) return fail(FC_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return FC_OK;
+}
+
+void free_run(fc_run *r) {
+    if (!r) return;
+    void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
+                    r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc, r->d_edge_since,
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    if (r->ev0) (void)hipEventDestroy(r->ev0);
+    if (r->ev1) (void)hipEventDestroy(r->ev1);
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    delete r;
+}
+
+bool district_contiguous(const fc::HostGraph &g, const int8_t *a, int k, std::vector<int32_t> &q,
+                         std::vector<uint8_t> &seen) {
+    std::fill(seen.begin(), seen.end(), 0);
+    for (int d = 0; d < k; ++d) {
+        int32_t start = -1, size = 0;
+        for (int32_t u = 0; u < g.n; ++u)
+            if (a[u] == d) { if (start < 0) start = u; ++size; }
+        if (start < 0) continue;
+        q.clear();
+        q.push_back(start);
+        seen[start] = 1;
+        for (size_t h = 0; h < q.size(); ++h) {
+            const int32_t u = q[h];
+            for (int32_t j = g.row_ptr[u]; j < g.row_ptr[u + 1]; ++j) {
+                const int32_t w = g.col_idx[j];
+                if (a[w] == d && !seen[w]) { seen[w] = 1; q.push_back(w); }
+            }
+        }
+        if ((int32_t)q.size() != size) return false;
+    }
+    return true;
+}
+
+template <int RMAX>
+std::vector<fc::NodeRec<RMAX>> pack_records(const fc::HostGraph &g) {
+    std::vector<fc::NodeRec<RMAX>> recs(g.n);
+    for (int32_t v = 0; v < g.n; ++v) {
+        auto &r = recs[v];
+        std::memset(&r, 0, sizeof r);
+        r.meta = g.meta[v];
+        r.pop = g.pop[v];
+        r.deg = g.row_ptr[v + 1] - g.row_ptr[v];
+        for (int j = 0; j < RMAX; ++j) {
+            const uint32_t x = (uint32_t)g.ring[(size_t)v * g.ring_max + j] & 0xffffu;
+            r.ring[j >> 1] |= x << (16 * (j & 1));
+        }
+    }
+    return recs;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *fc_last_error(void) { return g_err.c_str(); }
+
+int fc_device_count(int32_t *n) {
+    if (!n) return fail(FC_ERR_ARG, "fc_device_count: null output");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *n = 0;
+        return fail(FC_ERR_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *n = c;
+    return FC_OK;
+}
+
+int fc_graph_create(int32_t n, const int32_t *row_ptr, const int32_t *col_idx, const int32_t *pop,
+                    const double *pos_xy, uint32_t flags, fc_graph **out) {
+    if (!out) return fail(FC_ERR_ARG, "fc_graph_create: null output");
+    *out = nullptr;
+    auto *g = new (std::nothrow) fc_graph();
+    if (!g) return fail(FC_ERR_NOMEM, "fc_graph_create: out of memory");
+    std::string err;
+    try {
+        err = fc::build_host_graph(n, row_ptr, col_idx, pop, pos_xy, flags, g->h);
+    } catch (const std::exception &ex) {
+        err = std::string("fc_graph_create: ") + ex.what();
+    }
+    if (!err.empty()) {
+        delete g;
+        return fail(err.rfind("graph: round-1", 0) == 0 ? FC_ERR_UNSUPPORTED : FC_ERR_ARG, err);
+    }
+    *out = g;
+    return FC_OK;
+}
+
+int fc_graph_get_info(const fc_graph *g, fc_graph_info *out) {
+    if (!g || !out) return fail(FC_ERR_ARG, "fc_graph_get_info: null argument");
+    out->n_nodes = g->h.n;
+    out->n_edges = g->h.n_edges;
+    out->ring_max = g->h.ring_max;
+    out->max_degree = g->h.max_degree;
+    out->n_exact = g->h.n_exact;
+    out->n_gamma = g->h.n_gamma;
+    out->planar = g->h.planar ? 1 : 0;
+    out->outer_simple = g->h.outer_simple ? 1 : 0;
+    return FC_OK;
+}
+
+int fc_graph_edges(const fc_graph *g, int32_t *eu, int32_t *ev) {
+    if (!g || !eu || !ev) return fail(FC_ERR_ARG, "fc_graph_edges: null argument");
+    std::copy(g->h.eu.begin(), g->h.eu.end(), eu);
+    std::copy(g->h.ev.begin(), g->h.ev.end(), ev);
+    return FC_OK;
+}
+
+int fc_graph_rings(const fc_graph *g, int32_t *ring, uint64_t *meta) {
+    if (!g || !ring || !meta) return fail(FC_ERR_ARG, "fc_graph_rings: null argument");
+    std::copy(g->h.ring.begin(), g->h.ring.end(), ring);
+    std::copy(g->h.meta.begin(), g->h.meta.end(), meta);
+    return FC_OK;
+}
+
+void fc_graph_destroy(fc_graph *g) { delete g; }
+
+int32_t fc_run_n_chains(const fc_run *r) { return r ? r->n_chains : 0; }
+
+int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, const int8_t *init_assign,
+                  const double *bases, fc_run **out) {
+    if (!out) return fail(FC_ERR_ARG, "fc_run_create: null output");
+    *out = nullptr;
+    if (!gr || !p || !init_assign || n_chains <= 0) return fail(FC_ERR_ARG, "fc_run_create: null argument or n_chains <= 0");
+    if (p->k != 2) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: round-1 kernels implement k == 2 (BI_SIGN)");
+    if (p->proposal != FC_PROPOSE_BI_SIGN) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: unsupported proposal");
+    const fc::HostGraph &g = gr->h;
+    const int32_t n = g.n, E = g.n_edges, R = g.ring_max, k = p->k;
+    if (p->pop_lo > INT32_MAX || p->pop_hi > INT32_MAX || p->pop_lo < INT32_MIN || p->pop_hi < INT32_MIN)
+        return fail(FC_ERR_UNSUPPORTED, "fc_run_create: population bounds must fit int32");
+    for (int64_t i = 0; i < (int64_t)n_chains * n; ++i)
+        if (init_assign[i] < 0 || init_assign[i] >= k) return fail(FC_ERR_ARG, "fc_run_create: district id out of range");
+
+    std::unique_ptr<fc_run, void (*)(fc_run *)> r(new (std::nothrow) fc_run(), free_run);
+    if (!r) return fail(FC_ERR_NOMEM, "fc_run_create: out of memory");
+    r->g = g;
+    r->p = *p;
+    r->labels.resize(k);
+    for (int i = 0; i < k; ++i) r->labels[i] = p->labels ? p->labels[i] : i;
+    r->p.labels = nullptr;
+    r->log1mp.resize(n + 1);
+    if (p->log1mp) {
+        std::copy(p->log1mp, p->log1mp + n + 1, r->log1mp.begin());
+    } else {
+        const double denom = std::pow((double)n, (double)k) - 1.0;
+        for (int32_t b = 0; b <= n; ++b) r->log1mp[b] = std::log(1.0 - (double)b / denom);
+    }
+    r->p.log1mp = nullptr;
+    r->n_chains = n_chains;
+    r->npad = (n + 15) & ~15;
+    r->words = (n + 63) / 64;
+    r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + 3 * r->words * 8;
+    r->chain_lds_bytes = (r->chain_lds_bytes + 15) & ~15;
+    if ((size_t)r->chain_lds_bytes * fc::kWavesPerBlock > 160 * 1024)
+        return fail(FC_ERR_UNSUPPORTED, "fc_run_create: graph too large for the wave-per-chain LDS layout");
+
+    // ---- host-side initial state (validated like MarkovChain.__init__ [gc-0.2]) ---------
+    std::vector<int8_t> assign((size_t)n_chains * r->npad, 0);
+    std::vector<uint8_t> fcnt((size_t)n_chains * r->npad, 0);
+    std::vector<fc::ChainScalars> sc(n_chains);
+    std::vector<uint64_t> thresh((size_t)n_chains * (2 * R + 1));
+    std::vector<int32_t> q;
+    std::vector<uint8_t> seen(n);
+    const bool want_hist = p->diag_mask & FC_DIAG_HIST, want_edges = p->diag_mask & FC_DIAG_EDGES,
+               want_flips = p->diag_mask & FC_DIAG_FLIPS;
+    std::vector<int64_t> cut_hist, nb_hist, part_sum;
+    if (want_hist) { cut_hist.assign((size_t)n_chains * (E + 1), 0); nb_hist.assign((size_t)n_chains * (n + 1), 0); }
+    if (want_flips) part_sum.assign((size_t)n_chains * n, 0);
+    for (int32_t c = 0; c < n_chains; ++c) {
+        const int8_t *a = init_assign + (size_t)c * n;
+        std::memcpy(&assign[(size_t)c * r->npad], a, n);
+        int64_t pops[fc::kMaxK] = {0, 0};
+        int32_t ng[fc::kMaxK] = {0, 0};
+        for (int32_t u = 0; u < n; ++u) {
+            pops[a[u]] += g.pop[u];
+            if (g.meta[u] & fc::kMetaGamma) ng[a[u]] += 1;
+        }
+        for (int d = 0; d < k; ++d)
+            if (pops[d] < p->pop_lo || pops[d] > p->pop_hi)
+                return fail(FC_ERR_INVALID_STATE, "chain " + std::to_string(c) +
+                                                      ": The given initial_state is not valid according is_valid (population).");
+        if (!district_contiguous(g, a, k, q, seen))
+            return fail(FC_ERR_INVALID_STATE, "chain " + std::to_string(c) +
+                                                  ": The given initial_state is not valid according is_valid (contiguity).");
+        int32_t cut = 0, nb = 0;
+        for (int32_t e = 0; e < E; ++e) cut += a[g.eu[e]] != a[g.ev[e]];
+        for (int32_t u = 0; u < n; ++u) {
+            int32_t f = 0;
+            for (int32_t j = g.row_ptr[u]; j < g.row_ptr[u + 1]; ++j) f += a[g.col_idx[j]] != a[u];
+            fcnt[(size_t)c * r->npad + u] = (uint8_t)f;
+            nb += f > 0;
+        }
+        fc::ChainScalars &s = sc[c];
+        std::memset(&s, 0, sizeof s);
+        s.cut = cut;
+        s.nb = nb;
+        s.pops[0] = (int32_t)pops[0];
+        s.pops[1] = (int32_t)pops[1];
+        s.ngamma[0] = ng[0];
+        s.ngamma[1] = ng[1];
+        s.last_flip = -1;
+        int64_t wait0 = 0;
+        if (p->diag_mask & FC_DIAG_WAIT) {
+            const uint32_t gid = p->chain_id_offset + (uint32_t)c;
+            fc::Words4 w = fc::philox4x32_10(0u, 0u, gid, 2u, (uint32_t)p->seed, (uint32_t)(p->seed >> 32));
+            wait0 = (int64_t)std::ceil(std::log(1.0 - fc::u53(w.x0, w.x1)) / r->log1mp[nb]) - 1;
+        }
+        s.wait_cur = wait0;
+        // yield #0 (the initial state) enters every per-yield sum
+        s.sum_cut = cut;
+        s.sum_nb = nb;
+        s.sum_cut2 = (int64_t)cut * cut;
+        s.sum_nb2 = (int64_t)nb * nb;
+        s.sum_wait = wait0;
+        if (want_hist) {
+            cut_hist[(size_t)c * (E + 1) + cut] = 1;
+            nb_hist[(size_t)c * (n + 1) + nb] = 1;
+        }
+        if (want_flips)
+            for (int32_t u = 0; u < n; ++u) part_sum[(size_t)c * n + u] = r->labels[a[u]];  // :219
+        const double base = bases ? bases[c] : p->base;
+        for (int dd = -R; dd <= R; ++dd) {
+            // cut_accept: random() < base ** (-(cut' - cut)), grid_chain_sec11.py:175,179
+            const double bound = std::pow(base, (double)(-dd));
+            uint64_t t;
+            if (!(bound < 1.0)) t = 1ull << 53;                     // always accepted
+            else if (!(bound > 0.0)) t = 0;
+            else t = (uint64_t)std::ceil(bound * 9007199254740992.0);
+            thresh[(size_t)c * (2 * R + 1) + (dd + R)] = t;
+        }
+    }
+
+    // ---- device ---------------------------------------------------------------------------
+    HIP_TRY(hipSetDevice(p->device));
+    HIP_TRY(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&r->ev0));
+    HIP_TRY(hipEventCreate(&r->ev1));
+    int rc;
+    if (R == 8) {
+        auto recs = pack_records<8>(g);
+        if ((rc = dalloc((fc::NodeRec<8> **)&r->d_graph, recs.size()))) return rc;
+        HIP_TRY(hipMemcpy(r->d_graph, recs.data(), recs.size() * sizeof(recs[0]), hipMemcpyHostToDevice));
+    } else {
+        auto recs = pack_records<16>(g);
+        if ((rc = dalloc((fc::NodeRec<16> **)&r->d_graph, recs.size()))) return rc;
+        HIP_TRY(hipMemcpy(r->d_graph, recs.data(), recs.size() * sizeof(recs[0]), hipMemcpyHostToDevice));
+    }
+    if ((rc = dalloc(&r->d_ring_eid, g.ring_eid.size()))) return rc;
+    HIP_TRY(hipMemcpy(r->d_ring_eid, g.ring_eid.data(), g.ring_eid.size() * 4, hipMemcpyHostToDevice));
+    if ((rc = dalloc(&r->d_assign, assign.size()))) return rc;
+    HIP_TRY(hipMemcpy(r->d_assign, assign.data(), assign.size(), hipMemcpyHostToDevice));
+    if ((rc = dalloc(&r->d_fcnt, fcnt.size()))) return rc;
+    HIP_TRY(hipMemcpy(r->d_fcnt, fcnt.data(), fcnt.size(), hipMemcpyHostToDevice));
+    if ((rc = dalloc(&r->d_sc, sc.size()))) return rc;
+    HIP_TRY(hipMemcpy(r->d_sc, sc.data(), sc.size() * sizeof(sc[0]), hipMemcpyHostToDevice));
+    if ((rc = dalloc(&r->d_thresh, thresh.size()))) return rc;
+    HIP_TRY(hipMemcpy(r->d_thresh, thresh.data(), thresh.size() * 8, hipMemcpyHostToDevice));
+    if ((rc = dalloc(&r->d_log1mp, r->log1mp.size()))) return rc;
+    HIP_TRY(hipMemcpy(r->d_log1mp, r->log1mp.data(), r->log1mp.size() * 8, hipMemcpyHostToDevice));
+    if ((rc = dalloc(&r->d_labels, r->labels.size()))) return rc;
+    HIP_TRY(hipMemcpy(r->d_labels, r->labels.data(), r->labels.size() * 4, hipMemcpyHostToDevice));
+    if (want_hist) {
+        if ((rc = dalloc(&r->d_cut_hist, cut_hist.size()))) return rc;
+        if ((rc = dalloc(&r->d_nb_hist, nb_hist.size()))) return rc;
+        HIP_TRY(hipMemcpy(r->d_cut_hist, cut_hist.data(), cut_hist.size() * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(r->d_nb_hist, nb_hist.data(), nb_hist.size() * 8, hipMemcpyHostToDevice));
+    }
+    if (want_edges) {
+        if ((rc = dalloc(&r->d_edge_acc, (size_t)n_chains * E))) return rc;
+        if ((rc = dalloc(&r->d_edge_since, (size_t)n_chains * E))) return rc;
+        HIP_TRY(hipMemset(r->d_edge_acc, 0, (size_t)n_chains * E * 8));
+        HIP_TRY(hipMemset(r->d_edge_since, 0, (size_t)n_chains * E * 8));
+    }
+    if (want_flips) {
+        if ((rc = dalloc(&r->d_num_flips, (size_t)n_chains * n))) return rc;
+        if ((rc = dalloc(&r->d_part_sum, (size_t)n_chains * n))) return rc;
+        if ((rc = dalloc(&r->d_last_flipped, (size_t)n_chains * n))) return rc;
+        HIP_TRY(hipMemset(r->d_num_flips, 0, (size_t)n_chains * n * 8));
+        HIP_TRY(hipMemset(r->d_last_flipped, 0, (size_t)n_chains * n * 8));
+        HIP_TRY(hipMemcpy(r->d_part_sum, part_sum.data(), part_sum.size() * 8, hipMemcpyHostToDevice));
+    }
+    if (p->trace_chains > 0 && p->trace_cap > 0) {
+        const int32_t tc = std::min(p->trace_chains, n_chains);
+        r->p.trace_chains = tc;
+        if ((rc = dalloc(&r->d_trace, (size_t)tc * p->trace_cap))) return rc;
+    } else {
+        r->p.trace_chains = 0;
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    *out = r.release();
+    return FC_OK;
+}
+
+int fc_run_set_tape(fc_run *r, const uint32_t *tape, int64_t n_draws) {
+    if (!r) return fail(FC_ERR_ARG, "fc_run_set_tape: null run");
+    HIP_TRY(hipSetDevice(r->p.device));
+    if (r->d_tape) { HIP_TRY(hipFree(r->d_tape)); r->d_tape = nullptr; }
+    r->tape_draws = 0;
+    if (!tape || n_draws <= 0) return FC_OK;
+    const size_t words = (size_t)r->n_chains * (size_t)n_draws * 6;
+    int rc;
+    if ((rc = dalloc(&r->d_tape, words))) return rc;
+    HIP_TRY(hipMemcpy(r->d_tape, tape, words * 4, hipMemcpyHostToDevice));
+    r->tape_draws = n_draws;
+    return FC_OK;
+}
+
+int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream) {
+    if (!r) return fail(FC_ERR_ARG, "fc_run_steps: null run");
+    if (n_steps < 0) return fail(FC_ERR_ARG, "fc_run_steps: n_steps must be >= 0");
+    if (n_steps == 0) return FC_OK;
+    HIP_TRY(hipSetDevice(r->p.device));
+    fc::KParams k{};
+    k.graph = r->d_graph;
+    k.ring_eid = r->d_ring_eid;
+    k.n = r->g.n;
+    k.n_edges = r->g.n_edges;
+    k.n_chains = r->n_chains;
+    k.k = r->p.k;
+    k.chain_lds_bytes = r->chain_lds_bytes;
+    k.words = r->words;
+    k.lemire_thresh = (uint32_t)((1ull << 32) % (uint64_t)r->g.n);
+    k.chain_id_offset = r->p.chain_id_offset;
+    k.seed_lo = (uint32_t)r->p.seed;
+    k.seed_hi = (uint32_t)(r->p.seed >> 32);
+    k.pop_lo = (int32_t)r->p.pop_lo;
+    k.pop_hi = (int32_t)r->p.pop_hi;
+    k.n_steps = n_steps;
+    k.max_draws = max_draws > 0 ? max_draws : 65536 * std::max<int64_t>(n_steps, 1);
+    k.assign = r->d_assign;
+    k.fcnt = r->d_fcnt;
+    k.sc = r->d_sc;
+    k.thresh = r->d_thresh;
+    k.log1mp = r->d_log1mp;
+    k.labels = r->d_labels;
+    k.diag = r->p.diag_mask;
+    k.flags = r->p.flags;
+    k.cut_hist = r->d_cut_hist;
+    k.nb_hist = r->d_nb_hist;
+    k.edge_acc = r->d_edge_acc;
+    k.edge_since = r->d_edge_since;
+    k.num_flips = r->d_num_flips;
+    k.part_sum = r->d_part_sum;
+    k.last_flipped = r->d_last_flipped;
+    k.trace = r->d_trace;
+    k.trace_chains = r->p.trace_chains;
+    k.trace_cap = r->p.trace_cap;
+    k.tape = r->d_tape;
+    k.tape_draws = r->tape_draws;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : r->stream;
+    HIP_TRY(hipEventRecord(r->ev0, s));
+    const int e = fc::launch_flip_k2(k, r->g.ring_max, s);
+    if (e != 0) return fail(FC_ERR_HIP, std::string("flip kernel launch: ") + hipGetErrorString((hipError_t)e));
+    HIP_TRY(hipEventRecord(r->ev1, s));
+    r->timed = true;
+    return FC_OK;
+}
+
+int fc_run_sync(fc_run *r) {
+    if (!r) return fail(FC_ERR_ARG, "fc_run_sync: null run");
+    HIP_TRY(hipSetDevice(r->p.device));
+    HIP_TRY(hipDeviceSynchronize());
+    return FC_OK;
+}
+
+int fc_run_last_ms(fc_run *r, float *ms) {
+    if (!r || !ms) return fail(FC_ERR_ARG, "fc_run_last_ms: null argument");
+    if (!r->timed) return fail(FC_ERR_ARG, "fc_run_last_ms: no launch recorded");
+    HIP_TRY(hipEventSynchronize(r->ev1));
+    HIP_TRY(hipEventElapsedTime(ms, r->ev0, r->ev1));
+    return FC_OK;
+}
+
+int fc_run_read_stats(fc_run *r, fc_chain_stats *out) {
+    if (!r || !out) return fail(FC_ERR_ARG, "fc_run_read_stats: null argument");
+    if (int rc = fc_run_sync(r)) return rc;
+    std::vector<fc::ChainScalars> sc(r->n_chains);
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    for (int32_t c = 0; c < r->n_chains; ++c) {
+        const fc::ChainScalars &s = sc[c];
+        fc_chain_stats &o = out[c];
+        o.steps = s.steps;
+        o.proposals = s.proposals;
+        o.draws = (int64_t)s.draw;
+        o.accepted = s.accepted;
+        o.inv_contig = s.inv_contig;
+        o.inv_pop = s.inv_pop;
+        o.sum_cut = s.sum_cut;
+        o.sum_nb = s.sum_nb;
+        o.sum_wait = s.sum_wait;
+        o.sum_cut2 = s.sum_cut2;
+        o.sum_nb2 = s.sum_nb2;
+        o.wait_cur = s.wait_cur;
+        o.bfs_calls = s.bfs_calls;
+        o.bfs_levels = s.bfs_levels;
+        o.cut = s.cut;
+        o.nb = s.nb;
+        o.last_flip = s.last_flip;
+        o.stuck = s.stuck;
+    }
+    return FC_OK;
+}
+
+int fc_run_read_state(fc_run *r, int8_t *assign_out) {
+    if (!r || !assign_out) return fail(FC_ERR_ARG, "fc_run_read_state: null argument");
+    if (int rc = fc_run_sync(r)) return rc;
+    std::vector<int8_t> a((size_t)r->n_chains * r->npad);
+    HIP_TRY(hipMemcpy(a.data(), r->d_assign, a.size(), hipMemcpyDeviceToHost));
+    for (int32_t c = 0; c < r->n_chains; ++c)
+        std::memcpy(assign_out + (size_t)c * r->g.n, &a[(size_t)c * r->npad], r->g.n);
+    return FC_OK;
+}
+
+int fc_run_read_trace(fc_run *r, int32_t chain, fc_record *out, int64_t cap, int64_t *len) {
+    if (!r || !out || !len) return fail(FC_ERR_ARG, "fc_run_read_trace: null argument");
+    if (chain < 0 || chain >= r->p.trace_chains) return fail(FC_ERR_ARG, "fc_run_read_trace: chain is not traced");
+    if (int rc = fc_run_sync(r)) return rc;
+    fc::ChainScalars s;
+    HIP_TRY(hipMemcpy(&s, r->d_sc + chain, sizeof s, hipMemcpyDeviceToHost));
+    const int64_t n = std::min<int64_t>({s.trace_len, r->p.trace_cap, cap});
+    HIP_TRY(hipMemcpy(out, r->d_trace + (size_t)chain * r->p.trace_cap, (size_t)n * sizeof(fc_record),
+                      hipMemcpyDeviceToHost));
+    *len = s.trace_len;
+    return FC_OK;
+}
+
+int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist) {
+    if (!r || !cut_hist || !nb_hist) return fail(FC_ERR_ARG, "fc_run_read_hist: null argument");
+    if (!r->d_cut_hist) return fail(FC_ERR_ARG, "fc_run_read_hist: FC_DIAG_HIST not enabled");
+    if (int rc = fc_run_sync(r)) return rc;
+    HIP_TRY(hipMemcpy(cut_hist, r->d_cut_hist, (size_t)r->n_chains * (r->g.n_edges + 1) * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(nb_hist, r->d_nb_hist, (size_t)r->n_chains * (r->g.n + 1) * 8, hipMemcpyDeviceToHost));
+    return FC_OK;
+}
+
+int fc_run_read_edges(fc_run *r, int64_t *cut_times) {
+    if (!r || !cut_times) return fail(FC_ERR_ARG, "fc_run_read_edges: null argument");
+    if (!r->d_edge_acc) return fail(FC_ERR_ARG, "fc_run_read_edges: FC_DIAG_EDGES not enabled");
+    if (int rc = fc_run_sync(r)) return rc;
+    const size_t E = r->g.n_edges, C = r->n_chains;
+    std::vector<int64_t> acc(C * E), since(C * E);
+    std::vector<int8_t> a(C * r->npad);
+    std::vector<fc::ChainScalars> sc(C);
+    HIP_TRY(hipMemcpy(acc.data(), r->d_edge_acc, acc.size() * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(since.data(), r->d_edge_since, since.size() * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(a.data(), r->d_assign, a.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < C; ++c) {
+        const int8_t *ac = &a[c * r->npad];
+        const int64_t T = sc[c].steps + 1;  // yields so far
+        for (size_t e = 0; e < E; ++e) {
+            const bool is_cut = ac[r->g.eu[e]] != ac[r->g.ev[e]];
+            cut_times[c * E + e] = acc[c * E + e] + (is_cut ? T - since[c * E + e] : 0);
+        }
+    }
+    return FC_OK;
+}
+
+int fc_run_read_flips(fc_run *r, int64_t *num_flips, int64_t *part_sum, int64_t *last_flipped) {
+    if (!r || !num_flips || !part_sum || !last_flipped) return fail(FC_ERR_ARG, "fc_run_read_flips: null argument");
+    if (!r->d_num_flips) return fail(FC_ERR_ARG, "fc_run_read_flips: FC_DIAG_FLIPS not enabled");
+    if (int rc = fc_run_sync(r)) return rc;
+    const size_t n = r->g.n, C = r->n_chains;
+    std::vector<int8_t> a(C * r->npad);
+    std::vector<fc::ChainScalars> sc(C);
+    HIP_TRY(hipMemcpy(num_flips, r->d_num_flips, C * n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(part_sum, r->d_part_sum, C * n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(last_flipped, r->d_last_flipped, C * n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(a.data(), r->d_assign, a.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < C; ++c) {
+        const int64_t T = sc[c].steps + 1;
+        for (size_t u = 0; u < n; ++u)  // grid_chain_sec11.py:416-418
+            if (last_flipped[c * n + u] == 0) part_sum[c * n + u] = T * r->labels[a[c * r->npad + u]];
+    }
+    return FC_OK;
+}
+
+void fc_run_destroy(fc_run *r) {
+    if (!r) return;
+    (void)hipSetDevice(r->p.device);
+    (void)hipDeviceSynchronize();
+    free_run(r);
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+// Internal structures shared by the host graph builder, the C-ABI layer and the kernels.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/flipchain.h"
+
+namespace fc {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;   // one chain per wave, 4 chains per 256-thread workgroup
+constexpr int kMaxK = 2;            // round-1 kernels: k = 2 (BI_SIGN)
+
+// meta word layout (also exported by fc_graph_rings)
+constexpr uint64_t kMetaLenMask = 0xffull;
+constexpr uint64_t kMetaExact = 1ull << 8;
+constexpr uint64_t kMetaGamma = 1ull << 9;
+constexpr int kMetaNbrShift = 16;
+constexpr int kMetaLinkShift = 32;
+
+// Device node record: everything one proposal needs about its node, in one cache sector.
+// ring[] holds int16 node ids packed two per u32, padded with the node itself.
+template <int RMAX>
+struct alignas(16) NodeRec {
+    uint64_t meta;
+    int32_t pop;
+    int32_t deg;
+    uint32_t ring[RMAX / 2];
+};
+static_assert(sizeof(NodeRec<8>) == 32, "NodeRec<8> must be 32 B");
+static_assert(sizeof(NodeRec<16>) == 48, "NodeRec<16> must be 48 B");
+
+struct HostGraph {
+    int32_t n = 0, n_edges = 0, ring_max = 8, max_degree = 0;
+    std::vector<int32_t> row_ptr, col_idx, pop;
+    std::vector<double> pos;          // [2n] or empty
+    std::vector<int32_t> eu, ev;      // canonical edges
+    std::vector<int32_t> ring;        // [n * ring_max]
+    std::vector<uint64_t> meta;       // [n]
+    std::vector<int32_t> ring_eid;    // [n * ring_max] edge id of neighbour entries, else -1
+    int32_t n_exact = 0, n_gamma = 0;
+    bool planar = false, outer_simple = false, connected = false;
+};
+
+// Builds rings / exactness (fc_graph.cpp).  Returns an error message or "".
+std::string build_host_graph(int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
+                             const int32_t *pop, const double *pos_xy, uint32_t flags, HostGraph &g);
+
+// Per-chain persistent scalars (device, one struct per chain).
+struct ChainScalars {
+    uint64_t draw;          // next draw index
+    int64_t steps, proposals, accepted, inv_contig, inv_pop;
+    int64_t sum_cut, sum_nb, sum_wait, sum_cut2, sum_nb2;
+    int64_t wait_cur;
+    int64_t bfs_calls, bfs_levels;
+    int64_t trace_len;
+    int32_t cut, nb;
+    int32_t pops[kMaxK];
+    int32_t ngamma[kMaxK];
+    int32_t last_flip;
+    int32_t stuck;
+    int32_t pad[2];
+};
+
+// Kernel parameters (passed by value).
+struct KParams {
+    const void *graph;          // NodeRec<RMAX>[n]
+    const int32_t *ring_eid;    // [n * RMAX] (FC_DIAG_EDGES)
+    int32_t n, n_edges, n_chains, k;
+    int32_t chain_lds_bytes;    // LDS bytes per chain
+    int32_t words;              // ceil(n / 64) bitmap words
+    uint32_t lemire_thresh;     // 2^32 mod n
+    uint32_t chain_id_offset;
+    uint32_t seed_lo, seed_hi;
+    int32_t pop_lo, pop_hi;
+    int64_t n_steps;            // steps to advance per chain in this launch
+    int64_t max_draws;          // per chain per launch
+    int8_t *assign;             // [n_chains * n]
+    uint8_t *fcnt;              // [n_chains * n] foreign-neighbour counts
+    ChainScalars *sc;           // [n_chains]
+    const uint64_t *thresh;     // [n_chains * (2*RMAX+1)] acceptance thresholds (U53 mantissa)
+    const double *log1mp;       // [n + 1]
+    const int32_t *labels;      // [k]
+    uint32_t diag;              // FC_DIAG_*
+    uint32_t flags;             // FC_FLAG_*
+    // optional diagnostics
+    int64_t *cut_hist;          // [n_chains * (E+1)]
+    int64_t *nb_hist;           // [n_chains * (n+1)]
+    int64_t *edge_acc;          // [n_chains * E]
+    int64_t *edge_since;        // [n_chains * E]
+    int64_t *num_flips;         // [n_chains * n]
+    int64_t *part_sum;          // [n_chains * n]
+    int64_t *last_flipped;      // [n_chains * n]
+    fc_record *trace;           // [trace_chains * trace_cap]
+    int32_t trace_chains;
+    int64_t trace_cap;
+    const uint32_t *tape;       // replay tape or null
+    int64_t tape_draws;
+};
+
+// Launch wrappers (fc_kernels.hip).  Return a hipError_t as int.
+int launch_flip_k2(const KParams &p, int ring_max, void *stream);
+int launch_init_fcnt(const KParams &p, int ring_max, void *stream);
+
+}  // namespace fc

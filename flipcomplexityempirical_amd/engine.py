@@ -1,0 +1,214 @@
+"""Batched multi-chain engine over the C-ABI: the MI355X replacement of the reference's
+``Partition`` + ``MarkovChain`` hot loop (``grid_chain_sec11.py:316-408``).
+
+``FlipGraph`` owns an ``fc_graph`` (CSR + link rings, built natively from a
+:class:`~flipcomplexityempirical_amd.graphs.GraphSpec`); ``FlipRun`` owns an ``fc_run``
+(``n_chains`` independent k=2 chains, one per wavefront on the device).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+from .graphs import GraphSpec, log1mp_table
+
+_P = ctypes.POINTER
+
+STAT_FIELDS = [f for f, _ in _lib.ChainStats._fields_]
+RECORD_DTYPE = np.dtype([("draw", "<i8"), ("v", "<i4"), ("flags", "<i4"), ("cut", "<i4"),
+                         ("nb", "<i4"), ("wait", "<i8")])
+
+
+def _p(arr, ct):
+    return arr.ctypes.data_as(_P(ct)) if arr is not None else _P(ct)()
+
+
+class FlipGraph:
+    """Native graph handle (``fc_graph_create``)."""
+
+    def __init__(self, spec: GraphSpec, use_positions: bool = True, exact: bool = True):
+        self.spec = spec
+        L = _lib.load()
+        self._row = np.ascontiguousarray(spec.row_ptr, dtype=np.int32)
+        self._col = np.ascontiguousarray(spec.col_idx, dtype=np.int32)
+        self._pop = np.ascontiguousarray(spec.pop, dtype=np.int32)
+        pos = None
+        if use_positions and spec.pos is not None:
+            pos = np.ascontiguousarray(spec.pos, dtype=np.float64).reshape(-1)
+        h = ctypes.c_void_p()
+        flags = 0 if exact else _lib.FC_GRAPH_NO_EXACT
+        check(L.fc_graph_create(spec.n, _p(self._row, ctypes.c_int32), _p(self._col, ctypes.c_int32),
+                                _p(self._pop, ctypes.c_int32), _p(pos, ctypes.c_double), flags,
+                                ctypes.byref(h)), "fc_graph_create")
+        self.handle = h
+        info = _lib.GraphInfo()
+        check(L.fc_graph_get_info(h, ctypes.byref(info)), "fc_graph_get_info")
+        self.info = {f: getattr(info, f) for f, _ in _lib.GraphInfo._fields_}
+
+    @property
+    def n(self) -> int:
+        return self.info["n_nodes"]
+
+    @property
+    def n_edges(self) -> int:
+        return self.info["n_edges"]
+
+    def edges(self) -> np.ndarray:
+        eu = np.zeros(self.n_edges, dtype=np.int32)
+        ev = np.zeros(self.n_edges, dtype=np.int32)
+        check(_lib.load().fc_graph_edges(self.handle, _p(eu, ctypes.c_int32), _p(ev, ctypes.c_int32)))
+        return np.stack([eu, ev], axis=1)
+
+    def rings(self):
+        R = self.info["ring_max"]
+        ring = np.zeros(self.n * R, dtype=np.int32)
+        meta = np.zeros(self.n, dtype=np.uint64)
+        check(_lib.load().fc_graph_rings(self.handle, _p(ring, ctypes.c_int32), _p(meta, ctypes.c_uint64)))
+        return ring.reshape(self.n, R), meta
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.load().fc_graph_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - GC timing
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class RunConfig:
+    k: int = 2
+    base: float = 1.0
+    pop_lo: int = 0
+    pop_hi: int = 2 ** 31 - 1
+    seed: int = 0
+    chain_id_offset: int = 0
+    diag_mask: int = _lib.FC_DIAG_WAIT
+    flags: int = 0
+    device: int = 0
+    trace_chains: int = 0
+    trace_cap: int = 0
+    labels: Sequence[int] = (-1, 1)
+
+
+class FlipRun:
+    """``n_chains`` chains on one GPU (``fc_run_create``).  ``init_assign`` is
+    ``[n_chains, n]`` (or ``[n]``, broadcast) district ids; ``bases`` optional per chain."""
+
+    def __init__(self, graph: FlipGraph, init_assign: np.ndarray, cfg: RunConfig,
+                 bases: Optional[Sequence[float]] = None, n_chains: Optional[int] = None,
+                 log1mp: Optional[np.ndarray] = None):
+        L = _lib.load()
+        self.graph = graph
+        self.cfg = cfg
+        a = np.asarray(init_assign, dtype=np.int8)
+        if a.ndim == 1:
+            a = np.broadcast_to(a, (n_chains or 1, a.shape[0]))
+        self.n_chains = int(a.shape[0])
+        self._init = np.ascontiguousarray(a)
+        if self._init.shape[1] != graph.n:
+            raise ValueError("init_assign must have one entry per node")
+        self._labels = np.ascontiguousarray(cfg.labels, dtype=np.int32)
+        self._log1mp = np.ascontiguousarray(log1mp if log1mp is not None else log1mp_table(graph.n, cfg.k),
+                                            dtype=np.float64)
+        self._bases = None if bases is None else np.ascontiguousarray(bases, dtype=np.float64)
+        if self._bases is not None and self._bases.shape[0] != self.n_chains:
+            raise ValueError("bases must have one entry per chain")
+        prm = _lib.Params(k=cfg.k, proposal=_lib.FC_PROPOSE_BI_SIGN, base=float(cfg.base),
+                          pop_lo=int(cfg.pop_lo), pop_hi=int(cfg.pop_hi), seed=int(cfg.seed),
+                          chain_id_offset=int(cfg.chain_id_offset), diag_mask=int(cfg.diag_mask),
+                          flags=int(cfg.flags), device=int(cfg.device), trace_chains=int(cfg.trace_chains),
+                          trace_cap=int(cfg.trace_cap), labels=_p(self._labels, ctypes.c_int32),
+                          log1mp=_p(self._log1mp, ctypes.c_double))
+        h = ctypes.c_void_p()
+        check(L.fc_run_create(graph.handle, ctypes.byref(prm), self.n_chains, _p(self._init, ctypes.c_int8),
+                              _p(self._bases, ctypes.c_double), ctypes.byref(h)), "fc_run_create")
+        self.handle = h
+        self._tape = None
+
+    # ---- stepping ---------------------------------------------------------------------
+    def steps(self, n_steps: int, max_draws: int = 0, stream: Optional[int] = None) -> "FlipRun":
+        check(_lib.load().fc_run_steps(self.handle, int(n_steps), int(max_draws),
+                                       ctypes.c_void_p(stream) if stream else None), "fc_run_steps")
+        return self
+
+    def set_tape(self, tape: Optional[np.ndarray], n_draws: int = 0):
+        """Replay: ``tape`` is ``[n_chains, n_draws * 6]`` u32."""
+        if tape is None:
+            check(_lib.load().fc_run_set_tape(self.handle, _P(ctypes.c_uint32)(), 0))
+            self._tape = None
+            return
+        t = np.ascontiguousarray(tape, dtype=np.uint32).reshape(self.n_chains, -1)
+        n_draws = t.shape[1] // 6
+        self._tape = t
+        check(_lib.load().fc_run_set_tape(self.handle, _p(t, ctypes.c_uint32), n_draws), "fc_run_set_tape")
+
+    def sync(self):
+        check(_lib.load().fc_run_sync(self.handle))
+
+    def last_ms(self) -> float:
+        ms = ctypes.c_float(0)
+        check(_lib.load().fc_run_last_ms(self.handle, ctypes.byref(ms)))
+        return float(ms.value)
+
+    # ---- readouts ---------------------------------------------------------------------
+    def stats(self) -> Dict[str, np.ndarray]:
+        arr = (_lib.ChainStats * self.n_chains)()
+        check(_lib.load().fc_run_read_stats(self.handle, arr), "fc_run_read_stats")
+        raw = np.ctypeslib.as_array(arr)
+        return {f: np.array(raw[f]) for f in STAT_FIELDS}
+
+    def state(self) -> np.ndarray:
+        out = np.zeros((self.n_chains, self.graph.n), dtype=np.int8)
+        check(_lib.load().fc_run_read_state(self.handle, _p(out, ctypes.c_int8)), "fc_run_read_state")
+        return out
+
+    def trace(self, chain: int = 0) -> np.ndarray:
+        cap = self.cfg.trace_cap
+        out = np.zeros(cap, dtype=RECORD_DTYPE)
+        n = ctypes.c_int64(0)
+        check(_lib.load().fc_run_read_trace(self.handle, chain, ctypes.cast(out.ctypes.data, _P(_lib.Record)),
+                                            cap, ctypes.byref(n)), "fc_run_read_trace")
+        if n.value > cap:
+            raise OverflowError(f"trace capacity {cap} exceeded ({n.value} records)")
+        return out[:n.value]
+
+    def hist(self):
+        E, n = self.graph.n_edges, self.graph.n
+        ch = np.zeros((self.n_chains, E + 1), dtype=np.int64)
+        nh = np.zeros((self.n_chains, n + 1), dtype=np.int64)
+        check(_lib.load().fc_run_read_hist(self.handle, _p(ch, ctypes.c_int64), _p(nh, ctypes.c_int64)))
+        return ch, nh
+
+    def cut_times(self) -> np.ndarray:
+        out = np.zeros((self.n_chains, self.graph.n_edges), dtype=np.int64)
+        check(_lib.load().fc_run_read_edges(self.handle, _p(out, ctypes.c_int64)))
+        return out
+
+    def flips(self):
+        n = self.graph.n
+        nf = np.zeros((self.n_chains, n), dtype=np.int64)
+        ps = np.zeros((self.n_chains, n), dtype=np.int64)
+        lf = np.zeros((self.n_chains, n), dtype=np.int64)
+        check(_lib.load().fc_run_read_flips(self.handle, _p(nf, ctypes.c_int64), _p(ps, ctypes.c_int64),
+                                            _p(lf, ctypes.c_int64)))
+        return nf, ps, lf
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.load().fc_run_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass

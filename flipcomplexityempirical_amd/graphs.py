@@ -1,0 +1,241 @@
+"""Host-side graph and initial-plan builders: the input side of the flip-walk hot path.
+
+These reproduce the lattices and start plans the reference drivers build before they
+construct the gerrychain ``Partition``:
+
+* ``sec11_graph`` / ``sec11_plan``   -- ``grid_chain_sec11.py:186-260``
+  (40x40 grid, 4 corner nodes removed, 4 corner diagonals added; plans by alignment).
+* ``frank_graph`` / ``frank_plan``   -- ``Frankenstein_chain.py:186-246``
+  (20x20 square grid glued to a triangular lattice along y = 0).
+* ``grid_graph`` / ``threshold_plan`` -- the C1 config (10x10 grid, plan ``x[0] >= 5``).
+
+Everything is converted to a :class:`GraphSpec` -- CSR adjacency with a canonical node
+order (sorted node keys), integer node populations and planar positions. The positions
+feed the native ring builder (``fc_graph_create``), which derives the per-node link rings
+used by the on-device contiguity test. networkx is only used here, on the host.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, Hashable, List, Optional, Sequence
+
+import numpy as np
+
+try:  # networkx is a host-side dependency of the builders only
+    import networkx as nx
+except ImportError:  # pragma: no cover - the image ships networkx
+    nx = None
+
+
+@dataclass
+class GraphSpec:
+    """CSR view of a node-labelled graph (canonical node order = ``nodes``)."""
+
+    nodes: List[Hashable]
+    row_ptr: np.ndarray  # int32 [n+1]
+    col_idx: np.ndarray  # int32 [2E], neighbours of each row sorted ascending
+    pop: np.ndarray  # int32 [n]
+    pos: Optional[np.ndarray] = None  # float64 [n, 2]
+    nx_graph: object = None
+    index: Dict[Hashable, int] = field(default_factory=dict)
+
+    @property
+    def n(self) -> int:
+        return len(self.nodes)
+
+    @property
+    def n_edges(self) -> int:
+        return int(self.col_idx.shape[0] // 2)
+
+    def edges(self) -> np.ndarray:
+        """Canonical edge list ``(u, v)`` with ``u < v`` in CSR order (the order of
+        per-edge statistics such as ``cut_times``)."""
+        out = []
+        for u in range(self.n):
+            for w in self.col_idx[self.row_ptr[u]:self.row_ptr[u + 1]]:
+                if w > u:
+                    out.append((u, int(w)))
+        return np.asarray(out, dtype=np.int32).reshape(-1, 2)
+
+    def neighbors(self, u: int) -> np.ndarray:
+        return self.col_idx[self.row_ptr[u]:self.row_ptr[u + 1]]
+
+    def degree(self) -> np.ndarray:
+        return np.diff(self.row_ptr).astype(np.int32)
+
+    def assignment_array(self, assignment: Dict[Hashable, int], labels: Sequence[int]) -> np.ndarray:
+        """Map a ``{node: label}`` plan to district ids (index into ``labels``) in canonical order."""
+        lut = {lab: i for i, lab in enumerate(labels)}
+        return np.asarray([lut[assignment[nd]] for nd in self.nodes], dtype=np.int8)
+
+
+def from_networkx(g, pop_attr: str = "population", pos: Optional[Dict] = None) -> GraphSpec:
+    """Build a :class:`GraphSpec` from a networkx graph (nodes sorted for a canonical order)."""
+    nodes = sorted(g.nodes())
+    index = {nd: i for i, nd in enumerate(nodes)}
+    n = len(nodes)
+    row_ptr = np.zeros(n + 1, dtype=np.int32)
+    cols: List[int] = []
+    for i, nd in enumerate(nodes):
+        nb = sorted(index[w] for w in g.neighbors(nd) if w != nd)
+        cols.extend(nb)
+        row_ptr[i + 1] = len(cols)
+    col_idx = np.asarray(cols, dtype=np.int32)
+    popv = np.asarray([int(g.nodes[nd].get(pop_attr, 1)) for nd in nodes], dtype=np.int32)
+    p = None
+    if pos is None:
+        attr = nx.get_node_attributes(g, "pos") if nx is not None else {}
+        if len(attr) == n:
+            pos = attr
+    if pos is not None:
+        p = np.asarray([pos[nd] for nd in nodes], dtype=np.float64).reshape(n, 2)
+    return GraphSpec(nodes=nodes, row_ptr=row_ptr, col_idx=col_idx, pop=popv, pos=p,
+                     nx_graph=g, index=index)
+
+
+# --------------------------------------------------------------------------------------
+# sec11 (grid_chain_sec11.py)
+# --------------------------------------------------------------------------------------
+SEC11_MU = 2.63815853  # grid_chain_sec11.py:33
+SEC11_BASES = [.1, 1 / SEC11_MU ** 2, .2, 1 / SEC11_MU, .8, 1, SEC11_MU, 4, SEC11_MU ** 2, 10]  # :34
+SEC11_POPS = [.01, .05, .1, .5, .9]  # :36
+SEC11_DIAGONALS = [((0, 1), (1, 0)), ((0, 38), (1, 39)), ((38, 0), (39, 1)), ((38, 39), (39, 38))]  # :236
+SEC11_CORNERS = [(0, 0), (0, 39), (39, 0), (39, 39)]  # :252
+
+
+def sec11_nx(gn: int = 20, k: int = 2):
+    """The sec11 lattice exactly as ``grid_chain_sec11.py:191,218,236,252`` builds it."""
+    g = nx.grid_graph([k * gn, k * gn])
+    for nd in g.nodes():
+        g.nodes[nd]["population"] = 1  # :218
+    g.add_edges_from(SEC11_DIAGONALS)
+    g.remove_nodes_from(SEC11_CORNERS)
+    return g
+
+
+def sec11_graph() -> GraphSpec:
+    g = sec11_nx()
+    return from_networkx(g, pos={nd: (float(nd[0]), float(nd[1])) for nd in g.nodes()})
+
+
+def sec11_plan(alignment: int, nodes: Optional[Sequence] = None) -> Dict:
+    """±1 start plan, ``grid_chain_sec11.py:195-214`` (corners dropped as at :254-260)."""
+    if nodes is None:
+        nodes = [(x, y) for x in range(40) for y in range(40) if (x, y) not in SEC11_CORNERS]
+    out = {}
+    for n in nodes:
+        if alignment == 0:
+            out[n] = 1 if n[0] > 19 else -1
+        elif alignment == 1:
+            out[n] = 1 if n[1] > 19 else -1
+        elif alignment == 2:
+            if n[0] > n[1]:
+                out[n] = 1
+            elif n[0] == n[1] and n[0] > 19:
+                out[n] = 1
+            else:
+                out[n] = -1
+        else:
+            raise ValueError("alignment must be 0, 1 or 2")
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# FRANK (Frankenstein_chain.py)
+# --------------------------------------------------------------------------------------
+FRANK_BASES = [.3, 1 / .3]  # Frankenstein_chain.py:34
+FRANK_POPS = [.05, .1, .5, .9]  # :36
+
+
+def frank_nx(m: int = 20):
+    """``Frankenstein_chain.py:186-195``: grid (shifted to y <= 0) composed with a triangular lattice."""
+    G = nx.grid_graph([m, m])
+    relabel = {x: (x[0], x[1] - m + 1) for x in G.nodes()}
+    G = nx.relabel_nodes(G, relabel)
+    H = nx.triangular_lattice_graph(m, 2 * m - 2)
+    F = nx.compose(G, H)
+    for nd in F.nodes():
+        F.nodes[nd]["population"] = 1
+    return F
+
+
+def frank_positions(F) -> Dict:
+    pos = {}
+    for nd in F.nodes():
+        p = F.nodes[nd].get("pos")
+        pos[nd] = (float(p[0]), float(p[1])) if p is not None else (float(nd[0]), float(nd[1]))
+    return pos
+
+
+def frank_graph(m: int = 20) -> GraphSpec:
+    F = frank_nx(m)
+    return from_networkx(F, pos=frank_positions(F))
+
+
+def frank_plan(alignment: int, nodes: Sequence, m: int = 20) -> Dict:
+    """``Frankenstein_chain.py:207-246``: start_plans = [diagonal, vertical, horizontal]."""
+    if alignment == 0:
+        inside = lambda x: 2 * x[0] - x[1] <= m - 3
+    elif alignment == 1:
+        inside = lambda x: x[0] < m / 2
+    elif alignment == 2:
+        inside = lambda x: x[1] < 0
+    else:
+        raise ValueError("alignment must be 0, 1 or 2")
+    return {n: (1 if inside(n) else -1) for n in nodes}
+
+
+# --------------------------------------------------------------------------------------
+# Generic lattices used by the BASELINE configs
+# --------------------------------------------------------------------------------------
+def grid_graph(nx_: int, ny: int) -> GraphSpec:
+    g = nx.grid_graph([nx_, ny])
+    for nd in g.nodes():
+        g.nodes[nd]["population"] = 1
+    return from_networkx(g, pos={nd: (float(nd[0]), float(nd[1])) for nd in g.nodes()})
+
+
+def threshold_plan(nodes: Sequence, axis: int, cut: float) -> Dict:
+    """±1 plan by ``node[axis] >= cut`` (C1: 10x10 grid, ``x[0] >= 5``)."""
+    return {n: (1 if n[axis] >= cut else -1) for n in nodes}
+
+
+def triangular_graph(m: int, n: int) -> GraphSpec:
+    H = nx.triangular_lattice_graph(m, n)
+    for nd in H.nodes():
+        H.nodes[nd]["population"] = 1
+    return from_networkx(H)
+
+
+# --------------------------------------------------------------------------------------
+# Known answers used by tests (host-side, networkx)
+# --------------------------------------------------------------------------------------
+def cut_and_boundary(spec: GraphSpec, assign: np.ndarray):
+    """(|cut edges|, |boundary nodes|, district populations) of a district-id array."""
+    e = spec.edges()
+    cut = assign[e[:, 0]] != assign[e[:, 1]]
+    bnodes = np.zeros(spec.n, dtype=bool)
+    bnodes[e[cut, 0]] = True
+    bnodes[e[cut, 1]] = True
+    k = int(assign.max()) + 1
+    pops = np.bincount(assign.astype(np.int64), weights=spec.pop, minlength=k).astype(np.int64)
+    return int(cut.sum()), int(bnodes.sum()), pops
+
+
+def population_bounds(total_pop: int, k: int, percent: float):
+    """gerrychain ``within_percent_of_ideal_population`` bounds [gc-0.2], used at
+    ``grid_chain_sec11.py:319``: ``((1-p)*ideal, (1+p)*ideal)`` with ``ideal = total/k``;
+    returned as the float pair and the equivalent inclusive integer pair."""
+    ideal = total_pop / k
+    lo = (1 - percent) * ideal
+    hi = (1 + percent) * ideal
+    return (lo, hi), (int(math.ceil(lo)), int(math.floor(hi)))
+
+
+def log1mp_table(n_nodes: int, k: int) -> np.ndarray:
+    """``log(1 - p)`` for ``p = |B| / (N**k - 1)``, |B| = 0..N -- the exact float pipeline of
+    ``geom_wait`` (``grid_chain_sec11.py:147-148``: Python true division of ints, then numpy's
+    legacy ``log(1.0 - p)``)."""
+    denom = n_nodes ** k - 1
+    return np.asarray([math.log(1.0 - (b / denom)) for b in range(n_nodes + 1)], dtype=np.float64)

@@ -1,0 +1,166 @@
+/*
+ * flipchain.h -- C-ABI of the MI355X-native flip-walk engine (libflipchain.so).
+ *
+ * This is the drop-in boundary for the reference's hot path: the gerrychain MarkovChain
+ * protocol as the reference drives it,
+ *
+ *   exp_chain = MarkovChain(slow_reversible_propose_bi,
+ *                           Validator([single_flip_contiguous, popbound]),
+ *                           accept=cut_accept, initial_state=grid_partition,
+ *                           total_steps=100000)          grid_chain_sec11.py:340-342
+ *   for part in exp_chain: ...                           grid_chain_sec11.py:366-402
+ *
+ * Each entry point below names the reference interface it replaces.  Plain pointers and
+ * sizes only; no C++ exceptions cross this boundary; every call returns an int status
+ * (FC_OK = 0, < 0 error) and leaves a thread-local message in fc_last_error().
+ *
+ * Threading: one fc_run per host thread at a time.  The library has no global mutable
+ * state besides the thread-local error string.  fc_run_steps is asynchronous on the given
+ * HIP stream (NULL = the run's own stream); every fc_run_read_* call synchronises.
+ *
+ * Ownership: fc_graph_create / fc_run_create copy all host arrays; the library owns its
+ * device buffers and frees them in *_destroy.
+ */
+#ifndef FLIPCHAIN_H
+#define FLIPCHAIN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FC_OK 0
+#define FC_ERR_ARG (-1)          /* bad argument (TypeError / IndexError analogues)        */
+#define FC_ERR_INVALID_STATE (-2) /* initial state not valid: MarkovChain raises ValueError */
+#define FC_ERR_HIP (-3)          /* HIP runtime failure or no GPU                           */
+#define FC_ERR_UNSUPPORTED (-4)  /* configuration outside what the kernels implement        */
+#define FC_ERR_NOMEM (-5)
+
+/* fc_graph_create flags */
+#define FC_GRAPH_NO_EXACT 0x1u   /* never trust the planar local contiguity rule            */
+
+/* fc_params.proposal */
+#define FC_PROPOSE_BI_SIGN 0     /* slow_reversible_propose_bi, grid_chain_sec11.py:132-145 */
+
+/* fc_params.diag_mask: per-yield driver diagnostics kept on the device
+ * (grid_chain_sec11.py:350-419).  The streaming sums are always kept.                    */
+#define FC_DIAG_WAIT 0x1u        /* geometric waits, geom_wait :147-148 -> wait.txt          */
+#define FC_DIAG_HIST 0x2u        /* per-chain histograms of |cut| and |B| over yields        */
+#define FC_DIAG_EDGES 0x4u       /* per-edge cut_times, :383-384                             */
+#define FC_DIAG_FLIPS 0x8u       /* per-node num_flips / part_sum / last_flipped, :396-400   */
+
+/* fc_params.flags */
+#define FC_FLAG_FORCE_BFS 0x1u   /* resolve every multi-run contiguity case by device BFS   */
+
+typedef struct fc_graph fc_graph;
+typedef struct fc_run fc_run;
+
+typedef struct fc_graph_info {
+    int32_t n_nodes;
+    int32_t n_edges;
+    int32_t ring_max;     /* entries per node record (8 or 16)                            */
+    int32_t max_degree;
+    int32_t n_exact;      /* nodes whose local contiguity rule is exact (k = 2)          */
+    int32_t n_gamma;      /* nodes on the outer face                                      */
+    int32_t planar;       /* positions given and no two edges cross                       */
+    int32_t outer_simple; /* outer face boundary is a simple cycle                        */
+} fc_graph_info;
+
+typedef struct fc_params {
+    int32_t k;                 /* districts; round 1 kernels: k == 2                        */
+    int32_t proposal;          /* FC_PROPOSE_*                                              */
+    double base;               /* cut_accept base when `bases` is NULL (:171-179, :279-280) */
+    int64_t pop_lo, pop_hi;    /* inclusive integer bounds equivalent to
+                                  within_percent_of_ideal_population (:319)                 */
+    uint64_t seed;             /* Philox key (DESIGN.md "Random stream")                    */
+    uint32_t chain_id_offset;  /* global id of local chain 0 (multi-GPU sharding)           */
+    uint32_t diag_mask;        /* FC_DIAG_*                                                 */
+    uint32_t flags;            /* FC_FLAG_*                                                 */
+    int32_t device;            /* HIP device ordinal                                        */
+    int32_t trace_chains;      /* chains 0..trace_chains-1 record per-proposal traces      */
+    int64_t trace_cap;         /* records per traced chain                                  */
+    const int32_t *labels;     /* [k] reference district labels (e.g. -1, 1); NULL = 0..k-1 */
+    const double *log1mp;      /* [n+1] log(1 - b/(N^k - 1)); NULL = computed in double     */
+} fc_params;
+
+/* Per-chain statistics.  "Yields" are the states a `for part in exp_chain` loop sees:
+ * the initial state plus one per valid step; every sum runs over all yields. */
+typedef struct fc_chain_stats {
+    int64_t steps;        /* valid steps (MarkovChain steps after the initial yield)      */
+    int64_t proposals;    /* proposals: draws that hit a boundary node                    */
+    int64_t draws;        /* raw random draws                                             */
+    int64_t accepted;
+    int64_t inv_contig;   /* rejected by single_flip_contiguous                           */
+    int64_t inv_pop;      /* rejected by the population bound                             */
+    int64_t sum_cut;      /* sum over yields of |cut_edges|       (rce)                   */
+    int64_t sum_nb;       /* sum over yields of |b_nodes|         (rbn)                   */
+    int64_t sum_wait;     /* sum over yields of geom              (wait.txt)              */
+    int64_t sum_cut2;
+    int64_t sum_nb2;
+    int64_t wait_cur;     /* geometric wait of the current state                          */
+    int64_t bfs_calls;    /* contiguity cases resolved by device BFS                      */
+    int64_t bfs_levels;
+    int32_t cut;          /* current |cut_edges|                                           */
+    int32_t nb;           /* current |b_nodes|                                             */
+    int32_t last_flip;    /* node flipped to create the current state (-1: initial)       */
+    int32_t stuck;        /* a launch hit max_draws before finishing its steps            */
+} fc_chain_stats;
+
+/* One record per proposal (trace mode), identical in layout to the oracle's. */
+typedef struct fc_record {
+    int64_t draw;
+    int32_t v;
+    int32_t flags;        /* 1 valid, 2 accepted, 4 invalid: contiguity, 8 invalid: pop   */
+    int32_t cut;          /* state after this proposal                                     */
+    int32_t nb;
+    int64_t wait;         /* geometric wait of the yielded state (valid proposals)        */
+} fc_record;
+
+/* ---- graph: replaces gerrychain Graph + the networkx lattice (:186-260) ------------ */
+/* CSR adjacency (symmetric, no self loops), node populations (Tally('population'),
+ * :299), optional planar positions [2n] from which the per-node link rings and the
+ * exactness of the local contiguity rule are derived. */
+int fc_graph_create(int32_t n, const int32_t *row_ptr, const int32_t *col_idx, const int32_t *pop,
+                    const double *pos_xy, uint32_t flags, fc_graph **out);
+int fc_graph_get_info(const fc_graph *g, fc_graph_info *out);
+/* Canonical edge list (u < v, CSR order): the order of cut_times / cut_edges. */
+int fc_graph_edges(const fc_graph *g, int32_t *eu, int32_t *ev);
+/* Debug export of the rings: entries [n * ring_max] (padded with the node itself) and
+ * meta [n] (bits 0-7 length, 8 exact, 9 outer-face, 16-31 neighbour mask, 32-47 link mask). */
+int fc_graph_rings(const fc_graph *g, int32_t *ring, uint64_t *meta);
+void fc_graph_destroy(fc_graph *g);
+
+/* ---- run: replaces Partition(graph, assignment, updaters) + MarkovChain(...) --------- */
+/* init_assign: [n_chains * n] district ids 0..k-1 (one initial plan per chain).
+ * bases: [n_chains] per-chain cut_accept base, or NULL for params->base.
+ * Validates every initial state like MarkovChain.__init__ (FC_ERR_INVALID_STATE). */
+int fc_run_create(const fc_graph *g, const fc_params *p, int32_t n_chains, const int8_t *init_assign,
+                  const double *bases, fc_run **out);
+/* Advance every chain by n_steps valid steps (the reference's step semantics: invalid
+ * proposals are re-drawn and not counted).  max_draws caps the draws per chain per call
+ * (<= 0: 64 * 1024 * n_steps); a capped chain sets stats.stuck.  Asynchronous. */
+int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream);
+/* Replay mode: chain c reads its random words from tape[c * n_draws * 6 ...] (6 u32 per
+ * draw: 4 proposal words, 2 geometric words) instead of Philox.  NULL detaches. */
+int fc_run_set_tape(fc_run *r, const uint32_t *tape, int64_t n_draws);
+int fc_run_sync(fc_run *r);
+/* Device time of the last fc_run_steps launch, from HIP events on its stream. */
+int fc_run_last_ms(fc_run *r, float *ms);
+int fc_run_read_stats(fc_run *r, fc_chain_stats *out);
+int fc_run_read_state(fc_run *r, int8_t *assign_out);
+int fc_run_read_trace(fc_run *r, int32_t chain, fc_record *out, int64_t cap, int64_t *len);
+int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist);      /* [c*(E+1)], [c*(n+1)] */
+int fc_run_read_edges(fc_run *r, int64_t *cut_times);                     /* [c*E], finalised     */
+/* num_flips / part_sum / last_flipped [c*n], finalised as grid_chain_sec11.py:416-418. */
+int fc_run_read_flips(fc_run *r, int64_t *num_flips, int64_t *part_sum, int64_t *last_flipped);
+int32_t fc_run_n_chains(const fc_run *r);
+void fc_run_destroy(fc_run *r);
+
+int fc_device_count(int32_t *n);
+const char *fc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,318 @@
+/*
+ * flipref.c -- TEST INFRASTRUCTURE ONLY (see flipref.h).  A deliberately plain CPU
+ * restatement of the reference flip chain: every per-step quantity is recomputed the
+ * obvious way (BFS contiguity, neighbour scans, per-yield loops), mirroring the
+ * reference's own per-step work, so that it can serve as the checker for the HIP path.
+ */
+#include "flipref.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------- Philox4x32-10 (Salmon et al., SC'11; Random123 constants) -------- */
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+void fr_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += PHILOX_W0; k1 += PHILOX_W1; }
+        uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+        uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* CPython random.random(): two 32-bit words a, b (Lib/random.py / _randommodule.c). */
+static double u53(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+/* ---------------- chain context ---------------------------------------------------- */
+typedef struct {
+    const fr_params *p;
+    int8_t *a;
+    int64_t *pops;
+    int32_t *stamp;     /* BFS visited stamps */
+    int32_t stamp_id;
+    int32_t *queue;
+    int32_t cut, nb;
+    int32_t n_edges;
+    int32_t *eu, *ev;   /* canonical edges (u < v, CSR order) */
+} ctx_t;
+
+static int in_boundary(const ctx_t *c, int32_t u) {
+    const fr_params *p = c->p;
+    for (int32_t j = p->row_ptr[u]; j < p->row_ptr[u + 1]; ++j)
+        if (c->a[p->col_idx[j]] != c->a[u]) return 1;
+    return 0;
+}
+
+/* single_flip_contiguous [gc-0.2] restated: old_nbrs = neighbours still in v's old
+ * district; empty => invalid; else every old neighbour must reach one fixed old neighbour
+ * through the old district with v removed (the canonical stream omits the random.choice
+ * of the start neighbour: the outcome does not depend on it). */
+static int flip_contiguous_ctx(ctx_t *c, int32_t v) {
+    const fr_params *p = c->p;
+    const int8_t A = c->a[v];
+    int32_t n_old = 0, start = -1;
+    for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) {
+        int32_t w = p->col_idx[j];
+        if (c->a[w] == A) { if (start < 0) start = w; ++n_old; }
+    }
+    if (n_old == 0) return 0;
+    if (n_old == 1) return 1;
+    if (++c->stamp_id == 0x7fffffff) { memset(c->stamp, 0, sizeof(int32_t) * (size_t)p->n); c->stamp_id = 1; }
+    const int32_t sid = c->stamp_id;
+    int32_t head = 0, tail = 0, found = 1;
+    c->stamp[v] = sid;       /* v is removed from the district */
+    c->stamp[start] = sid;
+    c->queue[tail++] = start;
+    /* count targets reached */
+    while (head < tail) {
+        int32_t u = c->queue[head++];
+        for (int32_t j = p->row_ptr[u]; j < p->row_ptr[u + 1]; ++j) {
+            int32_t w = p->col_idx[j];
+            if (c->a[w] != A || c->stamp[w] == sid) continue;
+            c->stamp[w] = sid;
+            c->queue[tail++] = w;
+        }
+    }
+    found = 0;
+    for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) {
+        int32_t w = p->col_idx[j];
+        if (c->a[w] == A && c->stamp[w] == sid) ++found;
+    }
+    return found == n_old;
+}
+
+int fr_flip_contiguous(int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
+                       const int8_t *assign, int32_t v) {
+    fr_params p; memset(&p, 0, sizeof p);
+    p.n = n; p.row_ptr = row_ptr; p.col_idx = col_idx;
+    ctx_t c; memset(&c, 0, sizeof c);
+    c.p = &p;
+    c.a = (int8_t *)assign;
+    c.stamp = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+    c.queue = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    int r = (c.stamp && c.queue) ? flip_contiguous_ctx(&c, v) : -2;
+    free(c.stamp); free(c.queue);
+    return r;
+}
+
+/* gerrychain contiguous(): every district induces a connected subgraph. */
+int fr_districts_contiguous(int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
+                            int32_t k, const int8_t *assign) {
+    int32_t *seen = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+    int32_t *q = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    if (!seen || !q) { free(seen); free(q); return -2; }
+    int ok = 1;
+    for (int32_t d = 0; d < k && ok; ++d) {
+        int32_t start = -1, size = 0;
+        for (int32_t u = 0; u < n; ++u) if (assign[u] == d) { if (start < 0) start = u; ++size; }
+        if (start < 0) continue; /* empty district: gerrychain would not list it */
+        int32_t head = 0, tail = 0;
+        seen[start] = 1; q[tail++] = start;
+        while (head < tail) {
+            int32_t u = q[head++];
+            for (int32_t j = row_ptr[u]; j < row_ptr[u + 1]; ++j) {
+                int32_t w = col_idx[j];
+                if (assign[w] == d && !seen[w]) { seen[w] = 1; q[tail++] = w; }
+            }
+        }
+        if (tail != size) ok = 0;
+    }
+    free(seen); free(q);
+    return ok;
+}
+
+static void draw_words(const fr_params *p, int64_t d, uint32_t purpose, uint32_t w[4]) {
+    if (p->tape && purpose != 2) {   /* the initial state's wait always comes from Philox */
+        const uint32_t *t = p->tape + 6 * d;
+        if (purpose == 0) { w[0] = t[0]; w[1] = t[1]; w[2] = t[2]; w[3] = t[3]; }
+        else { w[0] = t[4]; w[1] = t[5]; w[2] = 0; w[3] = 0; }
+        return;
+    }
+    uint32_t ctr[4] = {(uint32_t)(uint64_t)d, (uint32_t)((uint64_t)d >> 32), p->chain_id, purpose};
+    uint32_t key[2] = {(uint32_t)p->seed, (uint32_t)(p->seed >> 32)};
+    fr_philox4x32_10(ctr, key, w);
+}
+
+/* geom_wait (grid_chain_sec11.py:147-148): int(np.random.geometric(p, 1)) - 1 with the
+ * legacy inversion ceil(log(1 - U) / log(1 - p)), U = legacy random_sample(). */
+static int64_t geom_wait(const fr_params *p, int64_t d, uint32_t purpose, int32_t nb) {
+    if (!p->log1mp) return 0;
+    uint32_t w[4];
+    draw_words(p, d, purpose, w);
+    double U = u53(w[0], w[1]);
+    return (int64_t)ceil(log(1.0 - U) / p->log1mp[nb]) - 1;
+}
+
+/* One driver-loop iteration (grid_chain_sec11.py:366-402) for the yielded state. */
+static void yield_state(ctx_t *c, fr_stats *st, fr_outputs *o, int64_t t) {
+    const fr_params *p = c->p;
+    st->sum_cut += c->cut;
+    st->sum_cut2 += (double)c->cut * (double)c->cut;
+    st->sum_nb += c->nb;
+    st->sum_nb2 += (double)c->nb * (double)c->nb;
+    st->sum_wait += st->wait_cur;
+    if (o) {
+        if (o->cut_hist) o->cut_hist[c->cut] += 1;
+        if (o->nb_hist) o->nb_hist[c->nb] += 1;
+        if (o->cut_times)
+            for (int32_t e = 0; e < c->n_edges; ++e)
+                if (c->a[c->eu[e]] != c->a[c->ev[e]]) o->cut_times[e] += 1;
+        /* part.flips is stale on rejected steps: the update repeats for the last accepted
+         * node (grid_chain_sec11.py:396-400, App. A.6 quirk 1). */
+        if (st->last_flip >= 0 && o->num_flips) {
+            int32_t f = st->last_flip;
+            o->part_sum[f] -= (int64_t)p->labels[(int)c->a[f]] * (t - o->last_flipped[f]);
+            o->last_flipped[f] = t;
+            o->num_flips[f] += 1;
+        }
+    }
+}
+
+int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outputs *o) {
+    if (!p || !init_assign || !st || p->n <= 0 || p->k != 2 || !p->row_ptr || !p->col_idx || !p->pop)
+        return -2;
+    if (o && o->num_flips && (!o->part_sum || !o->last_flipped || !p->labels)) return -2;
+    const int32_t n = p->n;
+    memset(st, 0, sizeof *st);
+    st->last_flip = -1;
+
+    ctx_t c; memset(&c, 0, sizeof c);
+    c.p = p;
+    c.a = (int8_t *)malloc((size_t)n);
+    c.pops = (int64_t *)calloc((size_t)p->k, sizeof(int64_t));
+    c.stamp = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+    c.queue = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    c.n_edges = p->row_ptr[n] / 2;
+    c.eu = (int32_t *)malloc(sizeof(int32_t) * (size_t)(c.n_edges + 1));
+    c.ev = (int32_t *)malloc(sizeof(int32_t) * (size_t)(c.n_edges + 1));
+    int rc = 0;
+    if (!c.a || !c.pops || !c.stamp || !c.queue || !c.eu || !c.ev) { rc = -2; goto done; }
+    memcpy(c.a, init_assign, (size_t)n);
+    {
+        int32_t e = 0;
+        for (int32_t u = 0; u < n; ++u)
+            for (int32_t j = p->row_ptr[u]; j < p->row_ptr[u + 1]; ++j)
+                if (p->col_idx[j] > u) { c.eu[e] = u; c.ev[e] = p->col_idx[j]; ++e; }
+    }
+    for (int32_t u = 0; u < n; ++u) {
+        if (c.a[u] < 0 || c.a[u] >= p->k) { rc = -2; goto done; }
+        c.pops[(int)c.a[u]] += p->pop[u];
+    }
+    /* MarkovChain.__init__ validates the initial state [gc-0.2]. */
+    for (int32_t d = 0; d < p->k; ++d)
+        if (c.pops[d] < p->pop_lo || c.pops[d] > p->pop_hi) { rc = -1; goto done; }
+    if (fr_districts_contiguous(n, p->row_ptr, p->col_idx, p->k, c.a) != 1) { rc = -1; goto done; }
+
+    for (int32_t e = 0; e < c.n_edges; ++e) c.cut += c.a[c.eu[e]] != c.a[c.ev[e]];
+    for (int32_t u = 0; u < n; ++u) c.nb += in_boundary(&c, u);
+    if (o) {
+        if (o->cut_times) memset(o->cut_times, 0, sizeof(int64_t) * (size_t)c.n_edges);
+        if (o->cut_hist) memset(o->cut_hist, 0, sizeof(int64_t) * (size_t)(c.n_edges + 1));
+        if (o->nb_hist) memset(o->nb_hist, 0, sizeof(int64_t) * (size_t)(n + 1));
+        if (o->num_flips)
+            for (int32_t u = 0; u < n; ++u) {
+                o->num_flips[u] = 0; o->last_flipped[u] = 0;
+                o->part_sum[u] = p->labels[(int)c.a[u]];       /* grid_chain_sec11.py:219 */
+            }
+        o->trace_len = 0;
+    }
+
+    st->wait0 = geom_wait(p, 0, 2, c.nb);
+    st->wait_cur = st->wait0;
+    yield_state(&c, st, o, 0);                                   /* yield #0 = S0 */
+
+    const uint32_t thresh = (uint32_t)((0x100000000ull) % (uint64_t)n);
+    int64_t d = 0;
+    while (st->steps < p->n_steps) {
+        if ((p->max_draws > 0 && st->draws >= p->max_draws) || (p->tape && d >= p->tape_draws)) {
+            st->stuck = 1; rc = 1; break;
+        }
+        uint32_t w[4];
+        draw_words(p, d, 0, w);
+        const int64_t draw = d++;
+        st->draws += 1;
+        const uint64_t m = (uint64_t)w[0] * (uint64_t)n;
+        if ((uint32_t)m < thresh) continue;                   /* Lemire: exact uniform node */
+        const int32_t v = (int32_t)(m >> 32);
+        if (!in_boundary(&c, v)) continue;                      /* not in b_nodes_bi        */
+        st->proposals += 1;
+        const int8_t A = c.a[v], T = (int8_t)(1 - A);
+        int32_t flags = 0;
+        if (!flip_contiguous_ctx(&c, v)) {
+            st->inv_contig += 1; flags = 4;
+        } else {
+            for (int32_t dd = 0; dd < p->k; ++dd) {
+                int64_t pp = c.pops[dd] - (dd == A ? p->pop[v] : 0) + (dd == T ? p->pop[v] : 0);
+                if (pp < p->pop_lo || pp > p->pop_hi) { flags = 8; break; }
+            }
+            if (flags) st->inv_pop += 1;
+        }
+        if (flags) {
+            if (o && o->trace && o->trace_len < o->trace_cap) {
+                fr_record *r = &o->trace[o->trace_len++];
+                r->draw = draw; r->v = v; r->flags = flags; r->cut = c.cut; r->nb = c.nb; r->wait = 0;
+            }
+            continue;
+        }
+        /* valid step: cut_accept (grid_chain_sec11.py:171-179) */
+        st->steps += 1;
+        int32_t same = 0, other = 0;
+        for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) {
+            int8_t aw = c.a[p->col_idx[j]];
+            same += aw == A; other += aw == T;
+        }
+        const int32_t delta = same - other;                    /* cut(S') - cut(S)        */
+        const double bound = pow(p->base, (double)(-delta));
+        const double U = u53(w[1], w[2]);
+        const int acc = U < bound;
+        if (acc) {
+            int32_t before = in_boundary(&c, v), after;
+            for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) before += in_boundary(&c, p->col_idx[j]);
+            c.a[v] = T;
+            c.pops[A] -= p->pop[v];
+            c.pops[T] += p->pop[v];
+            c.cut += delta;
+            after = in_boundary(&c, v);
+            for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) after += in_boundary(&c, p->col_idx[j]);
+            c.nb += after - before;
+            st->accepted += 1;
+            st->last_flip = v;
+            st->wait_cur = geom_wait(p, draw, 1, c.nb);
+        }
+        yield_state(&c, st, o, st->steps);
+        if (o && o->trace && o->trace_len < o->trace_cap) {
+            fr_record *r = &o->trace[o->trace_len++];
+            r->draw = draw; r->v = v; r->flags = 1 | (acc ? 2 : 0); r->cut = c.cut; r->nb = c.nb;
+            r->wait = st->wait_cur;
+        }
+    }
+    st->cut = c.cut;
+    st->nb = c.nb;
+    if (o) {
+        if (o->final_assign) memcpy(o->final_assign, c.a, (size_t)n);
+        /* finalisation, grid_chain_sec11.py:416-418 (t = number of yields) */
+        if (o->num_flips) {
+            const int64_t T = st->steps + 1;
+            for (int32_t u = 0; u < n; ++u)
+                if (o->last_flipped[u] == 0) o->part_sum[u] = T * p->labels[(int)c.a[u]];
+        }
+    }
+done:
+    free(c.a); free(c.pops); free(c.stamp); free(c.queue); free(c.eu); free(c.ev);
+    return rc;
+}

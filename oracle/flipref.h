@@ -1,0 +1,107 @@
+/*
+ * flipref.h -- TEST INFRASTRUCTURE ONLY.  CPU restatement (plain C) of the reference's
+ * flip-walk step, used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * as the checker.  The product (flipcomplexityempirical_amd/) never links or calls this.
+ *
+ * Semantics restated (reference files under /root/reference):
+ *   proposal   slow_reversible_propose_bi   grid_chain_sec11.py:132-145
+ *   boundary   b_nodes_bi                   grid_chain_sec11.py:155-156
+ *   accept     cut_accept                   grid_chain_sec11.py:171-179
+ *   wait       geom_wait                    grid_chain_sec11.py:147-148
+ *   chain      MarkovChain(..., Validator([single_flip_contiguous, popbound]), cut_accept)
+ *                                           grid_chain_sec11.py:319,340-342   [gc-0.2]
+ *   driver     per-yield diagnostics        grid_chain_sec11.py:365-419
+ *
+ * Random stream (the shared canonical spec, see DESIGN.md "Random stream"): draw d of
+ * chain c uses Philox4x32-10(ctr = (lo32 d, hi32 d, c, 0), key = (lo32 seed, hi32 seed)).
+ * Node = Lemire multiply-shift of word 0 over N (exact: reject low < 2^32 mod N); a draw
+ * whose node is not a boundary node is not a proposal.  Acceptance U53 = CPython random()
+ * from words (1, 2).  The geometric wait of the state created by draw d uses purpose 1,
+ * the initial state's purpose 2 at d = 0; U53 from words (0, 1).
+ * A tape (6 u32 per draw: the 4 proposal words then the 2 geometric words) may replace
+ * Philox -- the replay mode; the initial state's wait still comes from Philox purpose 2.
+ *
+ * Parity pins: tests/test_oracle_golden.py (known answers of the reference's start plans,
+ * the 174 decoded end-state artifacts, the 174 wait.txt sums) -- see DESIGN.md.
+ */
+#ifndef FLIPREF_H
+#define FLIPREF_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fr_record {
+    int64_t draw;   /* draw index of this proposal                          */
+    int32_t v;      /* proposed node (canonical index)                      */
+    int32_t flags;  /* 1 valid, 2 accepted, 4 invalid: contiguity, 8 invalid: population */
+    int32_t cut;    /* |cut edges| of the state after this proposal           */
+    int32_t nb;     /* |boundary nodes| after this proposal                   */
+    int64_t wait;   /* geometric wait of the yielded state (valid proposals) */
+} fr_record;
+
+typedef struct fr_stats {
+    int64_t steps;       /* valid proposals = yields after the initial one         */
+    int64_t proposals;   /* draws that hit a boundary node                         */
+    int64_t draws;       /* raw draws                                              */
+    int64_t accepted;
+    int64_t inv_contig;
+    int64_t inv_pop;
+    int64_t sum_cut;     /* sums over all yields t = 0..steps (initial included)   */
+    int64_t sum_nb;
+    int64_t sum_wait;    /* == sum(waits) written to wait.txt                      */
+    double  sum_cut2;
+    double  sum_nb2;
+    int32_t cut;         /* current state                                          */
+    int32_t nb;
+    int64_t wait0;       /* geometric wait of the initial state                    */
+    int64_t wait_cur;    /* geometric wait of the current state                    */
+    int32_t last_flip;   /* node flipped to create the current state, -1 for S0    */
+    int32_t stuck;       /* 1 if max_draws was reached before n_steps              */
+} fr_stats;
+
+typedef struct fr_params {
+    int32_t n;                 /* nodes                                            */
+    const int32_t *row_ptr;    /* CSR [n+1]                                        */
+    const int32_t *col_idx;    /* CSR [2E]                                         */
+    const int32_t *pop;        /* [n] node populations                             */
+    int32_t k;                 /* districts (k == 2: BI_SIGN proposal)             */
+    const int32_t *labels;     /* [k] reference labels (e.g. -1, +1) for part_sum  */
+    double base;               /* cut_accept base                                  */
+    int64_t pop_lo, pop_hi;    /* inclusive integer population bounds              */
+    uint64_t seed;
+    uint32_t chain_id;
+    const uint32_t *tape;      /* NULL => Philox; else 6 words per draw            */
+    int64_t tape_draws;
+    int64_t n_steps;           /* valid steps to advance                           */
+    int64_t max_draws;         /* stuck cap (<=0: unlimited)                       */
+    const double *log1mp;      /* [n+1] log(1-|B|/(N^k-1)); NULL => waits are 0    */
+} fr_params;
+
+typedef struct fr_outputs {
+    fr_record *trace; int64_t trace_cap; int64_t trace_len;   /* nullable trace      */
+    int8_t *final_assign;                                     /* [n]                 */
+    int64_t *cut_hist;                                        /* [E+1] nullable      */
+    int64_t *nb_hist;                                         /* [n+1] nullable      */
+    int64_t *cut_times;                                       /* [E]   nullable      */
+    int64_t *num_flips, *part_sum, *last_flipped;             /* [n]   nullable      */
+} fr_outputs;
+
+/* 0 ok; -1 initial state invalid (ValueError in MarkovChain.__init__); -2 bad args;
+ * 1 stuck (max_draws reached).  init_assign holds district ids 0..k-1. */
+int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outputs *out);
+
+/* Reference validity checks on a full assignment (gerrychain contiguous() + Bounds). */
+int fr_districts_contiguous(int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
+                            int32_t k, const int8_t *assign);
+/* single_flip_contiguous restated: flipping v out of its district keeps it connected. */
+int fr_flip_contiguous(int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
+                       const int8_t *assign, int32_t v);
+
+void fr_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

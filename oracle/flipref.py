@@ -1,0 +1,418 @@
+"""TEST INFRASTRUCTURE ONLY -- the parity oracle for the flip-walk hot path.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker / the timed CPU baseline.  The product
+(``flipcomplexityempirical_amd``) never imports it.
+
+Three pieces:
+
+* :func:`philox4x32_10` -- numpy Philox4x32-10 (the canonical random stream).
+* :class:`CRef` -- ctypes binding of ``oracle/flipref.c`` (plain-C restatement, fast
+  enough for 1e5-1e6-step parity runs).
+* :class:`GcFaithfulChain` -- pure-Python restatement with gerrychain-0.2 data structures
+  (dict assignment copied per proposal, cut-edge sets of sorted tuples, ``b_nodes_bi``
+  set, networkx ``multi_source_dijkstra`` contiguity).  This is the "reference Python CPU
+  path" (``cpu_baseline.kind = "port"``) and the small-case cross-check of the C oracle.
+
+Citations (``/root/reference``): proposal ``grid_chain_sec11.py:132-145``; boundary
+``:155-156``; acceptance ``:171-179``; geometric wait ``:147-148``; chain/validator
+``:319,340-342``; driver diagnostics ``:365-419``.  gerrychain internals are restated
+from gerrychain 0.2.x (not vendored in the reference) and marked [gc-0.2].
+
+Parity pinning of this oracle: ``tests/test_oracle_golden.py``.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libflipref.so")
+
+MASK32 = np.uint64(0xFFFFFFFF)
+_M0, _M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+_W0, _W1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
+
+FLAG_VALID, FLAG_ACCEPTED, FLAG_INV_CONTIG, FLAG_INV_POP = 1, 2, 4, 8
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Vectorised Philox4x32-10; inputs broadcast, returns 4 uint32 arrays."""
+    c0, c1, c2, c3 = (np.asarray(x, dtype=np.uint64) & MASK32 for x in (c0, c1, c2, c3))
+    k0 = np.asarray(k0, dtype=np.uint64) & MASK32
+    k1 = np.asarray(k1, dtype=np.uint64) & MASK32
+    for r in range(10):
+        if r:
+            k0 = (k0 + _W0) & MASK32
+            k1 = (k1 + _W1) & MASK32
+        p0 = _M0 * c0
+        p1 = _M1 * c2
+        c0, c1, c2, c3 = ((p1 >> np.uint64(32)) ^ c1 ^ k0, p1 & MASK32,
+                          (p0 >> np.uint64(32)) ^ c3 ^ k1, p0 & MASK32)
+    return tuple(np.asarray(x, dtype=np.uint32) for x in (c0, c1, c2, c3))
+
+
+def draw_tape(seed: int, chain_id: int, n_draws: int, start: int = 0) -> np.ndarray:
+    """The canonical stream as an explicit tape: 6 u32 per draw (4 proposal words, then the
+    2 geometric-wait words of purpose 1)."""
+    d = np.arange(start, start + n_draws, dtype=np.uint64)
+    lo, hi = d & MASK32, d >> np.uint64(32)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    a = philox4x32_10(lo, hi, chain_id, 0, k0, k1)
+    g = philox4x32_10(lo, hi, chain_id, 1, k0, k1)
+    tape = np.stack([a[0], a[1], a[2], a[3], g[0], g[1]], axis=1)
+    return np.ascontiguousarray(tape.reshape(-1), dtype=np.uint32)
+
+
+def u53(a: int, b: int) -> float:
+    """CPython ``random.random()`` from two 32-bit words."""
+    return ((a >> 5) * 67108864.0 + (b >> 6)) * (1.0 / 9007199254740992.0)
+
+
+# --------------------------------------------------------------------------------------
+# ctypes binding of flipref.c
+# --------------------------------------------------------------------------------------
+class FrRecord(ctypes.Structure):
+    _fields_ = [("draw", ctypes.c_int64), ("v", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("cut", ctypes.c_int32), ("nb", ctypes.c_int32), ("wait", ctypes.c_int64)]
+
+
+RECORD_DTYPE = np.dtype([("draw", "<i8"), ("v", "<i4"), ("flags", "<i4"), ("cut", "<i4"),
+                         ("nb", "<i4"), ("wait", "<i8")])
+
+
+class FrStats(ctypes.Structure):
+    _fields_ = [("steps", ctypes.c_int64), ("proposals", ctypes.c_int64), ("draws", ctypes.c_int64),
+                ("accepted", ctypes.c_int64), ("inv_contig", ctypes.c_int64), ("inv_pop", ctypes.c_int64),
+                ("sum_cut", ctypes.c_int64), ("sum_nb", ctypes.c_int64), ("sum_wait", ctypes.c_int64),
+                ("sum_cut2", ctypes.c_double), ("sum_nb2", ctypes.c_double),
+                ("cut", ctypes.c_int32), ("nb", ctypes.c_int32),
+                ("wait0", ctypes.c_int64), ("wait_cur", ctypes.c_int64),
+                ("last_flip", ctypes.c_int32), ("stuck", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_P = ctypes.POINTER
+
+
+class FrParams(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("row_ptr", _P(ctypes.c_int32)), ("col_idx", _P(ctypes.c_int32)),
+                ("pop", _P(ctypes.c_int32)), ("k", ctypes.c_int32), ("labels", _P(ctypes.c_int32)),
+                ("base", ctypes.c_double), ("pop_lo", ctypes.c_int64), ("pop_hi", ctypes.c_int64),
+                ("seed", ctypes.c_uint64), ("chain_id", ctypes.c_uint32),
+                ("tape", _P(ctypes.c_uint32)), ("tape_draws", ctypes.c_int64),
+                ("n_steps", ctypes.c_int64), ("max_draws", ctypes.c_int64),
+                ("log1mp", _P(ctypes.c_double))]
+
+
+class FrOutputs(ctypes.Structure):
+    _fields_ = [("trace", _P(FrRecord)), ("trace_cap", ctypes.c_int64), ("trace_len", ctypes.c_int64),
+                ("final_assign", _P(ctypes.c_int8)), ("cut_hist", _P(ctypes.c_int64)),
+                ("nb_hist", _P(ctypes.c_int64)), ("cut_times", _P(ctypes.c_int64)),
+                ("num_flips", _P(ctypes.c_int64)), ("part_sum", _P(ctypes.c_int64)),
+                ("last_flipped", _P(ctypes.c_int64))]
+
+
+def build_lib(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH) or \
+            os.path.getmtime(LIB_PATH) < max(os.path.getmtime(os.path.join(HERE, f)) for f in ("flipref.c", "flipref.h")):
+        subprocess.run(["make", "-C", HERE, "-s"], check=True)
+    return LIB_PATH
+
+
+def _ptr(arr, ctype):
+    if arr is None:
+        return ctypes.POINTER(ctype)()
+    return arr.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+class CRef:
+    """The plain-C oracle.  ``run`` restates one chain from its initial state."""
+
+    def __init__(self, lib_path: Optional[str] = None):
+        path = lib_path or LIB_PATH
+        if not os.path.exists(path):
+            build_lib()
+        self.lib = ctypes.CDLL(path)
+        self.lib.fr_run.argtypes = [_P(FrParams), _P(ctypes.c_int8), _P(FrStats), _P(FrOutputs)]
+        self.lib.fr_run.restype = ctypes.c_int
+        self.lib.fr_flip_contiguous.argtypes = [ctypes.c_int32, _P(ctypes.c_int32), _P(ctypes.c_int32),
+                                                _P(ctypes.c_int8), ctypes.c_int32]
+        self.lib.fr_districts_contiguous.argtypes = [ctypes.c_int32, _P(ctypes.c_int32), _P(ctypes.c_int32),
+                                                     ctypes.c_int32, _P(ctypes.c_int8)]
+        self.lib.fr_philox4x32_10.argtypes = [_P(ctypes.c_uint32), _P(ctypes.c_uint32), _P(ctypes.c_uint32)]
+
+    def philox(self, ctr, key):
+        c = (ctypes.c_uint32 * 4)(*ctr)
+        k = (ctypes.c_uint32 * 2)(*key)
+        o = (ctypes.c_uint32 * 4)()
+        self.lib.fr_philox4x32_10(c, k, o)
+        return list(o)
+
+    def districts_contiguous(self, spec, assign: np.ndarray, k: int) -> bool:
+        a = np.ascontiguousarray(assign, dtype=np.int8)
+        return self.lib.fr_districts_contiguous(spec.n, _ptr(spec.row_ptr, ctypes.c_int32),
+                                                _ptr(spec.col_idx, ctypes.c_int32), k,
+                                                _ptr(a, ctypes.c_int8)) == 1
+
+    def flip_contiguous(self, spec, assign: np.ndarray, v: int) -> bool:
+        a = np.ascontiguousarray(assign, dtype=np.int8)
+        return self.lib.fr_flip_contiguous(spec.n, _ptr(spec.row_ptr, ctypes.c_int32),
+                                           _ptr(spec.col_idx, ctypes.c_int32), _ptr(a, ctypes.c_int8), v) == 1
+
+    def run(self, spec, init_assign: np.ndarray, *, base: float, pop_lo: int, pop_hi: int,
+            seed: int, chain_id: int, n_steps: int, k: int = 2, labels=(-1, 1),
+            log1mp: Optional[np.ndarray] = None, tape: Optional[np.ndarray] = None,
+            max_draws: int = 0, trace_cap: int = 0, want_hist: bool = False,
+            want_edges: bool = False, want_flips: bool = False) -> Dict:
+        n, E = spec.n, spec.n_edges
+        row_ptr = np.ascontiguousarray(spec.row_ptr, dtype=np.int32)
+        col_idx = np.ascontiguousarray(spec.col_idx, dtype=np.int32)
+        pop = np.ascontiguousarray(spec.pop, dtype=np.int32)
+        lab = np.ascontiguousarray(labels, dtype=np.int32)
+        init = np.ascontiguousarray(init_assign, dtype=np.int8)
+        l1 = None if log1mp is None else np.ascontiguousarray(log1mp, dtype=np.float64)
+        tp = None if tape is None else np.ascontiguousarray(tape, dtype=np.uint32)
+        p = FrParams(n=n, row_ptr=_ptr(row_ptr, ctypes.c_int32), col_idx=_ptr(col_idx, ctypes.c_int32),
+                     pop=_ptr(pop, ctypes.c_int32), k=k, labels=_ptr(lab, ctypes.c_int32),
+                     base=float(base), pop_lo=int(pop_lo), pop_hi=int(pop_hi), seed=int(seed),
+                     chain_id=int(chain_id), tape=_ptr(tp, ctypes.c_uint32),
+                     tape_draws=0 if tp is None else tp.shape[0] // 6,
+                     n_steps=int(n_steps), max_draws=int(max_draws), log1mp=_ptr(l1, ctypes.c_double))
+        trace = np.zeros(trace_cap, dtype=RECORD_DTYPE) if trace_cap else None
+        final = np.zeros(n, dtype=np.int8)
+        cut_hist = np.zeros(E + 1, dtype=np.int64) if want_hist else None
+        nb_hist = np.zeros(n + 1, dtype=np.int64) if want_hist else None
+        cut_times = np.zeros(E, dtype=np.int64) if want_edges else None
+        nf = np.zeros(n, dtype=np.int64) if want_flips else None
+        ps = np.zeros(n, dtype=np.int64) if want_flips else None
+        lf = np.zeros(n, dtype=np.int64) if want_flips else None
+        o = FrOutputs(trace=ctypes.cast(trace.ctypes.data, _P(FrRecord)) if trace is not None else _P(FrRecord)(),
+                      trace_cap=trace_cap, trace_len=0, final_assign=_ptr(final, ctypes.c_int8),
+                      cut_hist=_ptr(cut_hist, ctypes.c_int64), nb_hist=_ptr(nb_hist, ctypes.c_int64),
+                      cut_times=_ptr(cut_times, ctypes.c_int64), num_flips=_ptr(nf, ctypes.c_int64),
+                      part_sum=_ptr(ps, ctypes.c_int64), last_flipped=_ptr(lf, ctypes.c_int64))
+        st = FrStats()
+        rc = self.lib.fr_run(ctypes.byref(p), _ptr(init, ctypes.c_int8), ctypes.byref(st), ctypes.byref(o))
+        if rc == -1:
+            raise ValueError("The given initial_state is not valid according is_valid.")
+        if rc == -2:
+            raise RuntimeError("fr_run: bad arguments")
+        out = {"rc": rc, "stats": st.as_dict(), "final": final}
+        if trace is not None:
+            out["trace"] = trace[:o.trace_len].copy()
+        if want_hist:
+            out["cut_hist"], out["nb_hist"] = cut_hist, nb_hist
+        if want_edges:
+            out["cut_times"] = cut_times
+        if want_flips:
+            out["num_flips"], out["part_sum"], out["last_flipped"] = nf, ps, lf
+        return out
+
+
+# --------------------------------------------------------------------------------------
+# gerrychain-0.2-faithful pure-Python restatement ("reference Python CPU path")
+# --------------------------------------------------------------------------------------
+class _Partition:
+    """Partition [gc-0.2]: ``flip`` builds a child that copies the node->part dict and
+    rebuilds the affected part frozensets (O(N)); updaters are lazy and cached per object."""
+
+    __slots__ = ("graph", "assignment", "parts", "parent", "flips", "_cache", "_ups")
+
+    def __init__(self, graph, assignment=None, updaters=None, parent=None, flips=None):
+        self.graph = graph
+        self._cache = {}
+        if parent is None:
+            self.assignment = dict(assignment)
+            parts = {}
+            for nd, p in self.assignment.items():
+                parts.setdefault(p, set()).add(nd)
+            self.parts = {p: frozenset(s) for p, s in parts.items()}
+            self._ups = dict(updaters)
+            self.parent = None
+            self.flips = None
+        else:
+            self._ups = parent._ups
+            self.parent = parent
+            self.flips = flips
+            self.assignment = parent.assignment.copy()
+            self.assignment.update(flips)
+            parts = dict(parent.parts)
+            touched = set(flips.values()) | {parent.assignment[nd] for nd in flips}
+            for p in touched:
+                parts[p] = frozenset(nd for nd, q in self.assignment.items() if q == p)
+            self.parts = parts
+
+    def flip(self, flips):
+        return _Partition(self.graph, parent=self, flips=flips)
+
+    def __getitem__(self, key):
+        if key not in self._cache:
+            self._cache[key] = self._ups[key](self)
+        return self._cache[key]
+
+    def __len__(self):
+        return len(self.parts)
+
+
+def _cut_edges(partition):  # gerrychain.updaters.cut_edges [gc-0.2]
+    if partition.parent is None:
+        a = partition.assignment
+        return {tuple(sorted(e)) for e in partition.graph.edges if a[e[0]] != a[e[1]]}
+    parent_cut = partition.parent["cut_edges"]
+    a = partition.assignment
+    new_cuts, obsolete = set(), set()
+    for node in partition.flips:
+        for nb in partition.graph.neighbors(node):
+            e = tuple(sorted((node, nb)))
+            if a[node] != a[nb]:
+                new_cuts.add(e)
+            else:
+                obsolete.add(e)
+    return (parent_cut | new_cuts) - obsolete
+
+
+def _b_nodes_bi(partition):  # grid_chain_sec11.py:155-156
+    return {x[0] for x in partition["cut_edges"]}.union({x[1] for x in partition["cut_edges"]})
+
+
+def _population(partition):  # Tally('population') [gc-0.2], incremental from the parent
+    if partition.parent is None:
+        out = {}
+        for nd, p in partition.assignment.items():
+            out[p] = out.get(p, 0) + partition.graph.nodes[nd]["population"]
+        return out
+    out = dict(partition.parent["population"])
+    for nd, new in partition.flips.items():
+        pop = partition.graph.nodes[nd]["population"]
+        out[partition.parent.assignment[nd]] -= pop
+        out[new] = out.get(new, 0) + pop
+    return out
+
+
+def _single_flip_contiguous(partition):  # [gc-0.2] restated
+    import networkx as nx
+    graph, assignment = partition.graph, partition.assignment
+
+    def avoid(start, end, attrs):
+        return None if assignment[start] != assignment[end] else 1
+
+    for changed, _ in partition.flips.items():
+        old = partition.parent.assignment[changed]
+        old_nbrs = [nd for nd in graph.neighbors(changed) if assignment[nd] == old]
+        if not old_nbrs:
+            return False
+        start = old_nbrs[0]  # canonical stream: the choice does not change the outcome
+        for nbr in old_nbrs:
+            try:
+                nx.multi_source_dijkstra(graph, [nbr], target=start, weight=avoid)
+            except nx.NetworkXNoPath:
+                return False
+    return True
+
+
+class GcFaithfulChain:
+    """One k=2 chain restated with gerrychain 0.2 structures, driven by the canonical
+    stream (Philox or a tape): node-tape replay of ``slow_reversible_propose_bi``."""
+
+    def __init__(self, spec, plan: Dict, *, base: float, pop_bounds, seed: int, chain_id: int,
+                 log1mp: Optional[np.ndarray] = None, tape: Optional[np.ndarray] = None):
+        self.spec = spec
+        self.g = spec.nx_graph
+        self.base = base
+        self.lo, self.hi = pop_bounds  # float bounds, exactly as Bounds compares
+        self.seed, self.chain_id = seed, chain_id
+        self.log1mp = log1mp
+        self.tape = tape
+        self.labels = sorted(set(plan.values()))
+        ups = {"population": _population, "cut_edges": _cut_edges, "b_nodes": _b_nodes_bi}
+        self.state = _Partition(self.g, assignment=plan, updaters=ups)
+        self.d = 0
+        self.n = spec.n
+        self.thresh = (1 << 32) % self.n
+        self.stats = dict(steps=0, proposals=0, draws=0, accepted=0, inv_contig=0, inv_pop=0,
+                          sum_cut=0, sum_nb=0, sum_wait=0)
+        self.trace = []
+        self.wait = self._geom(0, 2)
+        self._yield()
+
+    def _words(self, d, purpose):
+        if self.tape is not None and purpose != 2:
+            t = self.tape[6 * d: 6 * d + 6]
+            return [int(x) for x in (t[:4] if purpose == 0 else t[4:6])]
+        w = philox4x32_10(d & 0xFFFFFFFF, d >> 32, self.chain_id, purpose,
+                          self.seed & 0xFFFFFFFF, self.seed >> 32)
+        return [int(x) for x in w]
+
+    def _geom(self, d, purpose):
+        if self.log1mp is None:
+            return 0
+        w = self._words(d, purpose)
+        U = u53(w[0], w[1])
+        nb = len(self.state["b_nodes"])
+        return int(math.ceil(math.log(1.0 - U) / self.log1mp[nb])) - 1
+
+    def _yield(self):
+        s = self.state
+        self.stats["sum_cut"] += len(s["cut_edges"])
+        self.stats["sum_nb"] += len(s["b_nodes"])
+        self.stats["sum_wait"] += self.wait
+
+    def _valid(self, proposal):
+        if not _single_flip_contiguous(proposal):
+            return FLAG_INV_CONTIG
+        vals = proposal["population"].values()
+        if not (self.lo <= min(vals) and max(vals) <= self.hi):
+            return FLAG_INV_POP
+        return 0
+
+    def step(self):
+        """Advance one valid step (MarkovChain.__next__ [gc-0.2])."""
+        while True:
+            draw = self.d
+            w = self._words(draw, 0)
+            self.d += 1
+            self.stats["draws"] += 1
+            m = w[0] * self.n
+            if (m & 0xFFFFFFFF) < self.thresh:
+                continue
+            node = self.spec.nodes[m >> 32]
+            s = self.state
+            if node not in s["b_nodes"]:
+                continue
+            self.stats["proposals"] += 1
+            proposal = s.flip({node: -1 * s.assignment[node]})  # :145 (labels are ±1)
+            s.parent = None  # MarkovChain.__next__ erases the grandparent [gc-0.2]
+            bad = self._valid(proposal)
+            if bad:
+                self.stats["inv_contig" if bad == FLAG_INV_CONTIG else "inv_pop"] += 1
+                self.trace.append((draw, self.spec.index[node], bad, len(s["cut_edges"]), len(s["b_nodes"]), 0))
+                continue
+            self.stats["steps"] += 1
+            bound = self.base ** (-len(proposal["cut_edges"]) + len(s["cut_edges"]))  # :175
+            acc = u53(w[1], w[2]) < bound
+            if acc:
+                self.state = proposal
+                self.stats["accepted"] += 1
+                self.wait = self._geom(draw, 1)
+            self._yield()
+            cur = self.state
+            self.trace.append((draw, self.spec.index[node], FLAG_VALID | (FLAG_ACCEPTED if acc else 0),
+                               len(cur["cut_edges"]), len(cur["b_nodes"]), self.wait))
+            return cur
+
+    def run(self, n_steps: int):
+        for _ in range(n_steps):
+            self.step()
+        return self
+
+    def assignment_ids(self):
+        lut = {lab: i for i, lab in enumerate(self.labels)}
+        return np.asarray([lut[self.state.assignment[nd]] for nd in self.spec.nodes], dtype=np.int8)

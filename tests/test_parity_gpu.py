@@ -1,0 +1,141 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle, bit-exact.
+
+Every comparison is per proposal -- (draw, node, valid/accepted/invalid-reason, |cut|,
+|B|, geometric wait) -- plus final assignments, counters and all per-yield diagnostics.
+Both sides consume the same canonical random stream (DESIGN.md "Random stream").
+"""
+import numpy as np
+import pytest
+
+from flipcomplexityempirical_amd import graphs as G
+from flipcomplexityempirical_amd import _lib
+from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+
+pytestmark = pytest.mark.gpu
+
+STAT_KEYS = ["steps", "proposals", "draws", "accepted", "inv_contig", "inv_pop", "sum_cut", "sum_nb",
+             "sum_wait", "cut", "nb"]
+ALL_DIAG = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
+
+
+def _configs(spec, plan_fn, bases, n_chains):
+    inits, bs = [], []
+    for c in range(n_chains):
+        al = c % 3
+        inits.append(spec.assignment_array(plan_fn(al, spec.nodes), [-1, 1]))
+        bs.append(bases[(c // 3) % len(bases)])
+    return np.stack(inits), np.asarray(bs)
+
+
+def _run_gpu(spec, inits, bases, *, steps, chunks=1, seed=11, pct=0.1, flags=0, diag=ALL_DIAG,
+             trace_cap=200000, exact=True, tape=None):
+    fg = FlipGraph(spec, exact=exact)
+    (_, _), (lo, hi) = G.population_bounds(int(spec.pop.sum()), 2, pct)
+    cfg = RunConfig(seed=seed, pop_lo=lo, pop_hi=hi, diag_mask=diag, flags=flags,
+                    trace_chains=inits.shape[0], trace_cap=trace_cap)
+    run = FlipRun(fg, inits, cfg, bases=bases)
+    if tape is not None:
+        run.set_tape(tape)
+    per = steps // chunks
+    for i in range(chunks):
+        run.steps(per if i < chunks - 1 else steps - per * (chunks - 1))
+    return fg, run
+
+
+def _check_chain(cref, spec, run, c, init, base, *, steps, seed=11, pct=0.1, tape=None, diag=True):
+    (_, _), (lo, hi) = G.population_bounds(int(spec.pop.sum()), 2, pct)
+    ref = cref.run(spec, init, base=base, pop_lo=lo, pop_hi=hi, seed=seed, chain_id=c, n_steps=steps,
+                   log1mp=G.log1mp_table(spec.n, 2), trace_cap=500000, want_hist=diag, want_edges=diag,
+                   want_flips=diag, tape=tape)
+    st = run.stats()
+    tr = run.trace(c)
+    rt = ref["trace"]
+    assert len(tr) == len(rt), f"chain {c}: {len(tr)} vs {len(rt)} proposals"
+    for f in ("draw", "v", "flags", "cut", "nb", "wait"):
+        bad = np.nonzero(tr[f] != rt[f])[0]
+        assert bad.size == 0, f"chain {c} field {f} first mismatch at proposal {bad[:1]}: {tr[bad[:3]]} vs {rt[bad[:3]]}"
+    for k in STAT_KEYS:
+        assert int(st[k][c]) == int(ref["stats"][k]), f"chain {c} stat {k}: {st[k][c]} vs {ref['stats'][k]}"
+    assert np.array_equal(run.state()[c], ref["final"])
+    return ref
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_sec11_trace_parity(gpu, cref, sec11, chunks):
+    inits, bases = _configs(sec11, G.sec11_plan, G.SEC11_BASES, 30)
+    _, run = _run_gpu(sec11, inits, bases, steps=3000, chunks=chunks)
+    ch, nh = run.hist()
+    ct = run.cut_times()
+    nf, ps, lf = run.flips()
+    for c in range(inits.shape[0]):
+        ref = _check_chain(cref, sec11, run, c, inits[c], bases[c], steps=3000)
+        assert np.array_equal(ch[c], ref["cut_hist"])
+        assert np.array_equal(nh[c], ref["nb_hist"])
+        assert np.array_equal(ct[c], ref["cut_times"])
+        assert np.array_equal(nf[c], ref["num_flips"])
+        assert np.array_equal(lf[c], ref["last_flipped"])
+        assert np.array_equal(ps[c], ref["part_sum"])
+
+
+def test_sec11_force_bfs_parity(gpu, cref, sec11):
+    """Device BFS instead of the exact planar rule: identical trajectories."""
+    inits, bases = _configs(sec11, G.sec11_plan, [0.1, 1.0, G.SEC11_MU], 9)
+    _, run = _run_gpu(sec11, inits, bases, steps=1500, flags=_lib.FC_FLAG_FORCE_BFS)
+    st = run.stats()
+    assert st["bfs_calls"].sum() > 0
+    for c in range(inits.shape[0]):
+        _check_chain(cref, sec11, run, c, inits[c], bases[c], steps=1500)
+
+
+def test_sec11_no_positions_bfs_parity(gpu, cref, sec11):
+    """Rings without an embedding (no exactness): local rule + BFS fallback."""
+    inits, bases = _configs(sec11, G.sec11_plan, [0.2, 1.0, 4.0], 6)
+    _, run = _run_gpu(sec11, inits, bases, steps=1000, exact=False)
+    for c in range(inits.shape[0]):
+        _check_chain(cref, sec11, run, c, inits[c], bases[c], steps=1000)
+
+
+def test_frank_trace_parity(gpu, cref, frank):
+    inits, bases = _configs(frank, G.frank_plan, G.FRANK_BASES, 12)
+    _, run = _run_gpu(frank, inits, bases, steps=3000, pct=0.05)
+    ct = run.cut_times()
+    for c in range(inits.shape[0]):
+        ref = _check_chain(cref, frank, run, c, inits[c], bases[c], steps=3000, pct=0.05)
+        assert np.array_equal(ct[c], ref["cut_times"])
+
+
+def test_tape_replay_matches_philox(gpu, cref, sec11):
+    """Replay mode: a tape holding the Philox words reproduces the native run, and an
+    arbitrary tape is replayed identically by the oracle."""
+    from oracle.flipref import draw_tape
+    inits, bases = _configs(sec11, G.sec11_plan, [1.0, 10.0], 4)
+    n_draws = 60000
+    tapes = np.stack([draw_tape(11, c, n_draws) for c in range(4)])
+    _, run_t = _run_gpu(sec11, inits, bases, steps=1000, tape=tapes)
+    _, run_p = _run_gpu(sec11, inits, bases, steps=1000)
+    for c in range(4):
+        assert np.array_equal(run_t.trace(c), run_p.trace(c))
+    rng = np.random.default_rng(5)
+    wild = rng.integers(0, 2 ** 32, size=(4, n_draws * 6), dtype=np.uint64).astype(np.uint32)
+    _, run_w = _run_gpu(sec11, inits, bases, steps=800, tape=wild)
+    for c in range(4):
+        _check_chain(cref, sec11, run_w, c, inits[c], bases[c], steps=800, tape=wild[c])
+
+
+def test_c1_grid10(gpu, cref):
+    """BASELINE config C1: 10x10 grid, plan x[0] >= 5, base 1, pop tolerance 0.1."""
+    spec = G.grid_graph(10, 10)
+    init = spec.assignment_array(G.threshold_plan(spec.nodes, 0, 5), [-1, 1])[None, :]
+    _, run = _run_gpu(spec, init, np.asarray([1.0]), steps=20000)
+    _check_chain(cref, spec, run, 0, init[0], 1.0, steps=20000)
+
+
+def test_invalid_initial_state_raises(gpu, sec11):
+    fg = FlipGraph(sec11)
+    a = sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1]).copy()
+    a[sec11.index[(0, 5)]] = 1  # island of +1 inside -1: not contiguous
+    with pytest.raises(ValueError):
+        FlipRun(fg, a[None, :], RunConfig(pop_lo=0, pop_hi=10 ** 6))
+    with pytest.raises(ValueError):
+        FlipRun(fg, sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1])[None, :],
+                RunConfig(pop_lo=799, pop_hi=10 ** 6))
