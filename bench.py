@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Headline benchmark: flip proposals/s on the 40x40 sec11 grid, k = 2 (BASELINE.json).
+
+Workload (BASELINE config C2, the largest single-GPU configuration of the metric):
+the exact sec11 graph of ``grid_chain_sec11.py:186-260`` (N = 1596, E = 3116), 4096
+independent chains per GPU, chain c (global id g) with base ``bases[g % 10]``
+(``grid_chain_sec11.py:34``), start plan alignment ``(g // 10) % 3`` (``:195-214``),
+population tolerance 0.1 (``:319``), Philox seed 0x5EED0002.  One bench "step" is one
+launch advancing every chain by ``--chain-steps`` valid steps (default 10,000; 10 timed
+steps = the reference's 100,000-step run length).  Inputs are resident in HBM before the
+timed region; the timed region is bracketed by barrier + device synchronisation.
+
+N > 1 (``torch.distributed.run``): one process per GPU, chains sharded by global id with
+no data-path collective (weak scaling); one RCCL all-reduce of the statistics at the end.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "flip proposals/sec (node) 40x40 grid k=2, 1/2/4/8 MI355X; % LDS/HBM roofline"
+SEED = 0x5EED0002
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md chip-level parameters (spec)
+LDS_PEAK_GBS = 150000.0         # MI355X_MICROARCH.md §LDS: ~150 TB/s ds_read_b64/b128 aggregate
+# Algorithmic bytes: per proposal R = 2 + 1 + 8 + 5*deg + 5*L + 8 and per
+# accepted proposal W = 1 + 8 + 4*(deg+1) + 4 with deg = 4, L = 4 (sec11 interior).
+R_BYTES = 2 + 1 + 8 + 5 * 4 + 5 * 4 + 8      # 59
+W_BYTES = 1 + 8 + 4 * (4 + 1) + 4            # 33
+
+
+def _dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return None, 0, 1, int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    backend = "nccl" if torch.cuda.is_available() else "gloo"
+    dist.init_process_group(backend=backend)
+    return dist, dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def _cpu_worker(args):
+    """One chain of the same workload on the gerrychain-faithful Python port."""
+    gid, seconds = args
+    sys.path.insert(0, ROOT)
+    from flipcomplexityempirical_amd import graphs as G
+    from oracle.flipref import GcFaithfulChain
+    spec = G.sec11_graph()
+    plan = G.sec11_plan((gid // 10) % 3, spec.nodes)
+    (lo, hi), _ = G.population_bounds(spec.n, 2, 0.1)
+    ch = GcFaithfulChain(spec, plan, base=G.SEC11_BASES[gid % 10], pop_bounds=(lo, hi), seed=SEED,
+                         chain_id=gid, log1mp=G.log1mp_table(spec.n, 2))
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(20):
+            ch.step()
+    dt = time.perf_counter() - t0
+    return ch.stats["proposals"], ch.stats["steps"], dt
+
+
+def cpu_baseline(seconds: float, cores: int):
+    from concurrent.futures import ProcessPoolExecutor
+    with ProcessPoolExecutor(max_workers=cores) as ex:
+        res = list(ex.map(_cpu_worker, [(g, seconds) for g in range(cores)]))
+    props = sum(r[0] for r in res)
+    wall = max(r[2] for r in res)
+    return {"value": props / wall, "unit": "proposals/s", "cores": cores, "kind": "port",
+            "sample": f"gerrychain-0.2-faithful Python restatement (oracle/flipref.py GcFaithfulChain), "
+                      f"{cores} processes x 1 chain of the same workload (chain ids 0..{cores - 1}) for "
+                      f"{seconds:.0f} s each from the start plans; {props} proposals"}
+
+
+def c_oracle_rate(seconds: float):
+    """Single-core rate of the plain-C oracle on the same workload (extra, informational)."""
+    from flipcomplexityempirical_amd import graphs as G
+    from oracle.flipref import CRef
+    spec = G.sec11_graph()
+    cref = CRef()
+    _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
+    l1 = G.log1mp_table(spec.n, 2)
+    props, t0, g = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        a0 = spec.assignment_array(G.sec11_plan((g // 10) % 3, spec.nodes), [-1, 1])
+        r = cref.run(spec, a0, base=G.SEC11_BASES[g % 10], pop_lo=lo, pop_hi=hi, seed=SEED, chain_id=g,
+                     n_steps=20000, log1mp=l1)
+        props += r["stats"]["proposals"]
+        g += 1
+    return props / (time.perf_counter() - t0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--chain-steps", type=int, default=10000)
+    ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    dist, rank, world, local_rank = _dist()
+    import torch
+    from flipcomplexityempirical_amd import graphs as G
+    from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+
+    spec = G.sec11_graph()
+    fg = FlipGraph(spec)
+    C = args.chains
+    gids = np.arange(rank * C, (rank + 1) * C)
+    plans = [spec.assignment_array(G.sec11_plan(al, spec.nodes), [-1, 1]) for al in range(3)]
+    inits = np.stack([plans[(g // 10) % 3] for g in gids])
+    bases = np.asarray([G.SEC11_BASES[g % 10] for g in gids])
+    _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
+    cfg = RunConfig(seed=SEED, pop_lo=lo, pop_hi=hi, chain_id_offset=int(rank * C), device=local_rank)
+    run = FlipRun(fg, inits, cfg, bases=bases)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+
+    def barrier_sync():
+        run.sync()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        run.steps(args.chain_steps)
+    barrier_sync()
+    s0 = run.stats()
+    run.timings()  # reset the per-launch event record
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run.steps(args.chain_steps)
+    barrier_sync()
+    t1 = time.perf_counter()
+    launch_ms = run.timings()
+    s1 = run.stats()
+
+    elapsed = t1 - t0
+    props = float((s1["proposals"] - s0["proposals"]).sum())
+    steps = float((s1["steps"] - s0["steps"]).sum())
+    acc = float((s1["accepted"] - s0["accepted"]).sum())
+    kernel_ms = float(launch_ms.mean()) if launch_ms.size else float("nan")
+
+    if dist is not None:
+        dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+        t = torch.tensor([props, steps, acc], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        m = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        props, steps, acc = (float(x) for x in t.tolist())
+        elapsed, kernel_ms = (float(x) for x in m.tolist())
+        # the one collective of the statistics themselves: per-base sums
+        agg = np.zeros((10, 6), dtype=np.float64)
+        for b in range(10):
+            sel = (gids % 10) == b
+            agg[b] = [s1["proposals"][sel].sum(), s1["steps"][sel].sum(), s1["accepted"][sel].sum(),
+                      s1["sum_cut"][sel].sum(), s1["sum_nb"][sel].sum(), s1["sum_wait"][sel].sum()]
+        ta = torch.tensor(agg, device=dev)
+        dist.all_reduce(ta, op=dist.ReduceOp.SUM)
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    value = props / elapsed
+    per_launch_props = props / world / args.steps
+    per_launch_acc = acc / world / args.steps
+    alg_bytes = R_BYTES * per_launch_props + W_BYTES * per_launch_acc
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("chains") == C and tj.get("chain_steps") == args.chain_steps:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC, "value": value, "unit": "proposals/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "data": "synthetic: the reference's sec11 lattice and start plans, Philox stream",
+        "config": {"workload": "C2: sec11 40x40 grid (N=1596, E=3116), k=2, 4096 chains/GPU, "
+                               "base bases[g%10], alignment (g//10)%3, pop tol 0.1, seed 0x5EED0002",
+                   "graph": "sec11", "k": 2, "chains_per_gpu": C, "chain_steps_per_launch": args.chain_steps,
+                   "parallelism": f"chains sharded over {world} GPU(s)"},
+        "steps_per_s": steps / elapsed,
+        "accept_per_proposal": acc / props if props else None,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "flip_k2_kernel<8>", "kernel_ms": kernel_ms,
+                     "alg_bytes_per_launch": alg_bytes,
+                     "lds": {"peak": LDS_PEAK_GBS, "frac": achieved / LDS_PEAK_GBS}},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        cores = min(16, os.cpu_count() or 1)
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cores)
+            out["cpu_baseline_c_oracle_1core"] = c_oracle_rate(min(5.0, args.cpu_seconds))
+        except Exception as ex:  # report, never fake
+            out["cpu_baseline"] = {"value": None, "error": repr(ex)}
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -26,7 +26,7 @@ FC_FLAG_FORCE_BFS = 0x1
 
 EXPORTED = [
     "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
-    "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_sync", "fc_run_last_ms",
+    "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
     "fc_run_read_stats", "fc_run_read_state", "fc_run_read_trace", "fc_run_read_hist",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_n_chains", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
@@ -99,6 +99,7 @@ def load(build_if_missing: bool = True):
     L.fc_run_set_tape.argtypes = [vp, _P(ctypes.c_uint32), i64]
     L.fc_run_sync.argtypes = [vp]
     L.fc_run_last_ms.argtypes = [vp, _P(ctypes.c_float)]
+    L.fc_run_timings.argtypes = [vp, _P(ctypes.c_float), i32, _P(i32)]
     L.fc_run_read_stats.argtypes = [vp, _P(ChainStats)]
     L.fc_run_read_state.argtypes = [vp, _P(ctypes.c_int8)]
     L.fc_run_read_trace.argtypes = [vp, i32, _P(Record), i64, _P(i64)]

@@ -29,6 +29,8 @@ struct fc_run {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> launch_events;  // pool
+    size_t n_launch_events = 0;                                      // recorded since last read
     // device buffers
     void *d_graph = nullptr;
     int32_t *d_ring_eid = nullptr;
@@ -77,8 +79,7 @@ void free_run(fc_run *r) {
                     r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
-    if (r->ev0) (void)hipEventDestroy(r->ev0);
-    if (r->ev1) (void)hipEventDestroy(r->ev1);
+    for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
 }
@@ -308,8 +309,6 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     // ---- device ---------------------------------------------------------------------------
     HIP_TRY(hipSetDevice(p->device));
     HIP_TRY(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreate(&r->ev0));
-    HIP_TRY(hipEventCreate(&r->ev1));
     int rc;
     if (R == 8) {
         auto recs = pack_records<8>(g);
@@ -423,10 +422,20 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.tape = r->d_tape;
     k.tape_draws = r->tape_draws;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : r->stream;
-    HIP_TRY(hipEventRecord(r->ev0, s));
+    if (r->n_launch_events == r->launch_events.size()) {
+        hipEvent_t a, b;
+        HIP_TRY(hipEventCreate(&a));
+        HIP_TRY(hipEventCreate(&b));
+        r->launch_events.emplace_back(a, b);
+    }
+    auto &evp = r->launch_events[r->n_launch_events];
+    HIP_TRY(hipEventRecord(evp.first, s));
     const int e = fc::launch_flip_k2(k, r->g.ring_max, s);
     if (e != 0) return fail(FC_ERR_HIP, std::string("flip kernel launch: ") + hipGetErrorString((hipError_t)e));
-    HIP_TRY(hipEventRecord(r->ev1, s));
+    HIP_TRY(hipEventRecord(evp.second, s));
+    r->ev0 = evp.first;
+    r->ev1 = evp.second;
+    ++r->n_launch_events;
     r->timed = true;
     return FC_OK;
 }
@@ -443,6 +452,21 @@ int fc_run_last_ms(fc_run *r, float *ms) {
     if (!r->timed) return fail(FC_ERR_ARG, "fc_run_last_ms: no launch recorded");
     HIP_TRY(hipEventSynchronize(r->ev1));
     HIP_TRY(hipEventElapsedTime(ms, r->ev0, r->ev1));
+    return FC_OK;
+}
+
+int fc_run_timings(fc_run *r, float *ms, int32_t cap, int32_t *n) {
+    if (!r || !n || (cap > 0 && !ms)) return fail(FC_ERR_ARG, "fc_run_timings: null argument");
+    HIP_TRY(hipSetDevice(r->p.device));
+    const size_t cnt = r->n_launch_events;
+    if (cnt) HIP_TRY(hipEventSynchronize(r->launch_events[cnt - 1].second));
+    int32_t m = 0;
+    for (size_t i = 0; i < cnt && m < cap; ++i, ++m)
+        HIP_TRY(hipEventElapsedTime(&ms[m], r->launch_events[i].first, r->launch_events[i].second));
+    *n = (int32_t)cnt;
+    // keep the most recent pair at slot 0 so fc_run_last_ms stays valid
+    if (cnt > 1) std::swap(r->launch_events[0], r->launch_events[cnt - 1]);
+    r->n_launch_events = 0;
     return FC_OK;
 }
 

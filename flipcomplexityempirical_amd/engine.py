@@ -159,6 +159,13 @@ class FlipRun:
         check(_lib.load().fc_run_last_ms(self.handle, ctypes.byref(ms)))
         return float(ms.value)
 
+    def timings(self, cap: int = 4096) -> np.ndarray:
+        """Device ms of every launch since the previous call (HIP events on the run's stream)."""
+        out = np.zeros(cap, dtype=np.float32)
+        n = ctypes.c_int32(0)
+        check(_lib.load().fc_run_timings(self.handle, _p(out, ctypes.c_float), cap, ctypes.byref(n)))
+        return out[:min(n.value, cap)].astype(np.float64)
+
     # ---- readouts ---------------------------------------------------------------------
     def stats(self) -> Dict[str, np.ndarray]:
         arr = (_lib.ChainStats * self.n_chains)()

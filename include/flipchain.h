@@ -147,6 +147,9 @@ int fc_run_set_tape(fc_run *r, const uint32_t *tape, int64_t n_draws);
 int fc_run_sync(fc_run *r);
 /* Device time of the last fc_run_steps launch, from HIP events on its stream. */
 int fc_run_last_ms(fc_run *r, float *ms);
+/* Device times (ms) of every fc_run_steps launch since the previous call (up to cap;
+ * *n receives the count); synchronises on the last launch and resets the record. */
+int fc_run_timings(fc_run *r, float *ms, int32_t cap, int32_t *n);
 int fc_run_read_stats(fc_run *r, fc_chain_stats *out);
 int fc_run_read_state(fc_run *r, int8_t *assign_out);
 int fc_run_read_trace(fc_run *r, int32_t chain, fc_record *out, int64_t cap, int64_t *len);
