@@ -42,9 +42,12 @@ def _dist():
         return None, 0, 1, int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
-    backend = "nccl" if torch.cuda.is_available() else "gloo"
+    # FC_BENCH_BACKEND / FC_BENCH_DEVICE only serve rehearsals of the N > 1 path on a
+    # one-GPU box (several ranks on device 0 over gloo); the real run uses RCCL, one GPU per rank.
+    backend = os.environ.get("FC_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     dist.init_process_group(backend=backend)
-    return dist, dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("FC_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    return dist, dist.get_rank(), dist.get_world_size(), local
 
 
 def _cpu_worker(args):
@@ -114,13 +117,15 @@ def main():
 
     spec = G.sec11_graph()
     fg = FlipGraph(spec)
+    from flipcomplexityempirical_amd import distributed as D
     C = args.chains
-    gids = np.arange(rank * C, (rank + 1) * C)
+    off, cnt = D.shard(C * world, world, rank)          # weak scaling: C chains per GPU
+    gids = np.arange(off, off + cnt)
     plans = [spec.assignment_array(G.sec11_plan(al, spec.nodes), [-1, 1]) for al in range(3)]
     inits = np.stack([plans[(g // 10) % 3] for g in gids])
     bases = np.asarray([G.SEC11_BASES[g % 10] for g in gids])
     _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
-    cfg = RunConfig(seed=SEED, pop_lo=lo, pop_hi=hi, chain_id_offset=int(rank * C), device=local_rank)
+    cfg = RunConfig(seed=SEED, pop_lo=lo, pop_hi=hi, chain_id_offset=int(off), device=local_rank)
     run = FlipRun(fg, inits, cfg, bases=bases)
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
@@ -152,22 +157,15 @@ def main():
     acc = float((s1["accepted"] - s0["accepted"]).sum())
     kernel_ms = float(launch_ms.mean()) if launch_ms.size else float("nan")
 
-    if dist is not None:
-        dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
-        t = torch.tensor([props, steps, acc], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        m = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        props, steps, acc = (float(x) for x in t.tolist())
-        elapsed, kernel_ms = (float(x) for x in m.tolist())
-        # the one collective of the statistics themselves: per-base sums
-        agg = np.zeros((10, 6), dtype=np.float64)
-        for b in range(10):
-            sel = (gids % 10) == b
-            agg[b] = [s1["proposals"][sel].sum(), s1["steps"][sel].sum(), s1["accepted"][sel].sum(),
-                      s1["sum_cut"][sel].sum(), s1["sum_nb"][sel].sum(), s1["sum_wait"][sel].sum()]
-        ta = torch.tensor(agg, device=dev)
-        dist.all_reduce(ta, op=dist.ReduceOp.SUM)
+    # the one collective: per-base statistics summed over ranks (RCCL for N > 1)
+    dev = None
+    if dist is not None and dist.get_backend() == "nccl":
+        dev = torch.device("cuda", local_rank)
+    delta = {k: s1[k] - s0[k] for k in D.AGG_FIELDS}
+    agg = D.allreduce_sum(D.group_aggregate(delta, gids % 10, 10), dist, dev)
+    elapsed = D.allreduce_max(elapsed, dist, dev)
+    kernel_ms = D.allreduce_max(kernel_ms, dist, dev)
+    props, steps, acc = (float(agg[:, D.AGG_FIELDS.index(k)].sum()) for k in ("proposals", "steps", "accepted"))
 
     if rank != 0:
         if dist is not None:
@@ -198,6 +196,7 @@ def main():
                    "graph": "sec11", "k": 2, "chains_per_gpu": C, "chain_steps_per_launch": args.chain_steps,
                    "parallelism": f"chains sharded over {world} GPU(s)"},
         "steps_per_s": steps / elapsed,
+        "per_base_proposals_per_s": {f"{b:.4g}": float(agg[i, 0]) / elapsed for i, b in enumerate(G.SEC11_BASES)},
         "accept_per_proposal": acc / props if props else None,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -27,7 +27,7 @@ FC_FLAG_FORCE_BFS = 0x1
 EXPORTED = [
     "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
     "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
-    "fc_run_read_stats", "fc_run_read_state", "fc_run_read_trace", "fc_run_read_hist",
+    "fc_run_read_stats", "fc_run_read_state", "fc_run_read_trace", "fc_run_trace_reset", "fc_run_read_hist",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_n_chains", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
 ]
@@ -103,6 +103,7 @@ def load(build_if_missing: bool = True):
     L.fc_run_read_stats.argtypes = [vp, _P(ChainStats)]
     L.fc_run_read_state.argtypes = [vp, _P(ctypes.c_int8)]
     L.fc_run_read_trace.argtypes = [vp, i32, _P(Record), i64, _P(i64)]
+    L.fc_run_trace_reset.argtypes = [vp]
     L.fc_run_read_hist.argtypes = [vp, _P(i64), _P(i64)]
     L.fc_run_read_edges.argtypes = [vp, _P(i64)]
     L.fc_run_read_flips.argtypes = [vp, _P(i64), _P(i64), _P(i64)]

@@ -1,0 +1,477 @@
+"""gerrychain-shaped drop-in for the reference's chain construction and loop.
+
+The reference builds its chain as (``grid_chain_sec11.py:299-342``)::
+
+    updaters = {'population': Tally('population'), 'cut_edges': cut_edges,
+                'b_nodes': b_nodes_bi, 'base': new_base, 'geom': geom_wait, ...}
+    grid_partition = Partition(graph, assignment=cddict, updaters=updaters)
+    popbound = within_percent_of_ideal_population(grid_partition, pop1)
+    exp_chain = MarkovChain(slow_reversible_propose_bi,
+                            Validator([single_flip_contiguous, popbound]),
+                            accept=cut_accept, initial_state=grid_partition,
+                            total_steps=100000)
+    for part in exp_chain: ...
+
+The same lines run unchanged against this module.  ``MarkovChain`` compiles the
+recognised callables (by name: ``slow_reversible_propose_bi``, ``single_flip_contiguous``,
+``Bounds`` over ``population``, ``cut_accept`` / ``always_accept``) into device parameters
+and runs the chain on the GPU through the C-ABI.  Anything else raises
+``NotImplementedError``: there is no CPU fallback for the chain itself.
+
+Iterating a ``MarkovChain`` yields Partition-like views of every state (rejected steps
+re-yield the same object, as gerrychain does), reconstructed on the host from the device's
+per-proposal trace; ``MarkovChain.run()`` is the fast path that returns the driver's
+diagnostics (``wait.txt`` sum, ``cut_times``, ``num_flips``, ``part_sum`` ...) computed on
+the device.
+
+The host-side helpers (``Tally``, ``cut_edges``, ``b_nodes_bi``, ``Bounds``,
+``single_flip_contiguous``, ...) restate gerrychain 0.2 [gc-0.2] for direct calls on a
+``Partition``; they are not on the hot path.
+"""
+from __future__ import annotations
+
+import math
+import random
+from collections.abc import Mapping
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, Hashable, Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .graphs import GraphSpec, from_networkx, log1mp_table
+
+# ----------------------------------------------------------------------------------------
+# gerrychain updaters / constraints restated for host-side use  [gc-0.2]
+# ----------------------------------------------------------------------------------------
+
+
+class Tally:
+    """``gerrychain.updaters.Tally``: per-part sum of a node attribute."""
+
+    def __init__(self, fields, alias: Optional[str] = None):
+        self.fields = [fields] if isinstance(fields, str) else list(fields)
+        self.alias = alias
+
+    def __call__(self, partition):
+        out: Dict[Any, float] = {}
+        g = partition.graph
+        for nd, p in partition.assignment.items():
+            out[p] = out.get(p, 0) + sum(g.nodes[nd][f] for f in self.fields)
+        return out
+
+
+def cut_edges(partition):
+    """``gerrychain.updaters.cut_edges``: edges (sorted tuples) whose ends are in different parts."""
+    a = partition.assignment
+    return {tuple(sorted(e)) for e in partition.graph.edges if a[e[0]] != a[e[1]]}
+
+
+def b_nodes_bi(partition):
+    """``grid_chain_sec11.py:155-156``."""
+    return {x[0] for x in partition["cut_edges"]}.union({x[1] for x in partition["cut_edges"]})
+
+
+def b_nodes(partition):
+    """``grid_chain_sec11.py:151-153`` (node, neighbouring part) pairs."""
+    a = partition.assignment
+    return {(x[0], a[x[1]]) for x in partition["cut_edges"]}.union(
+        {(x[1], a[x[0]]) for x in partition["cut_edges"]})
+
+
+def geom_wait(partition):
+    """``grid_chain_sec11.py:147-148`` on numpy's global legacy stream (host use only; inside a
+    device chain the wait comes from the canonical stream)."""
+    p = len(list(partition["b_nodes"])) / (len(partition.graph.nodes) ** (len(partition.parts)) - 1)
+    return int(np.random.geometric(p, 1)) - 1
+
+
+class Bounds:
+    """``gerrychain.constraints.Bounds``: ``lower <= min(func(p))`` and ``max(func(p)) <= upper``."""
+
+    def __init__(self, func: Callable, bounds):
+        self.func = func
+        self.bounds = bounds
+
+    def __call__(self, partition) -> bool:
+        lower, upper = self.bounds
+        values = self.func(partition)
+        return lower <= min(values) and max(values) <= upper
+
+
+def within_percent_of_ideal_population(initial_partition, percent: float = 0.01, pop_key: str = "population"):
+    """[gc-0.2]: bounds ``((1-p)*ideal, (1+p)*ideal)`` fixed from the initial partition."""
+    number_of_districts = len(initial_partition[pop_key].keys())
+    total_population = sum(initial_partition[pop_key].values())
+    ideal_population = total_population / number_of_districts
+    bounds = ((1 - percent) * ideal_population, (1 + percent) * ideal_population)
+    b = Bounds(lambda partition: partition[pop_key].values(), bounds=bounds)
+    b.pop_key = pop_key
+    return b
+
+
+def contiguous(partition) -> bool:
+    """Every part induces a connected subgraph."""
+    import networkx as nx
+    for nodes in partition.parts.values():
+        if not nx.is_connected(partition.graph.subgraph(nodes)):
+            return False
+    return True
+
+
+def single_flip_contiguous(partition) -> bool:
+    """[gc-0.2] restated (BFS through the old district with the flipped node removed)."""
+    parent = partition.parent
+    if not parent:
+        return contiguous(partition)
+    graph, assignment = partition.graph, partition.assignment
+    for changed, _ in partition.flips.items():
+        old = parent.assignment[changed]
+        old_nbrs = [n for n in graph.neighbors(changed) if assignment[n] == old]
+        if not old_nbrs:
+            return False
+        seen, stack = {old_nbrs[0]}, [old_nbrs[0]]
+        while stack:
+            u = stack.pop()
+            for w in graph.neighbors(u):
+                if w not in seen and w != changed and assignment[w] == old:
+                    seen.add(w)
+                    stack.append(w)
+        if any(n not in seen for n in old_nbrs):
+            return False
+    return True
+
+
+class Validator:
+    """``gerrychain.constraints.Validator``: ordered AND; a non-bool result is a TypeError."""
+
+    def __init__(self, constraints):
+        self.constraints = list(constraints)
+
+    def __call__(self, partition) -> bool:
+        for c in self.constraints:
+            r = c(partition)
+            if r is False:
+                return False
+            if r is not True:
+                raise TypeError(f"Constraint {c!r} returned a non-boolean.")
+        return True
+
+
+def slow_reversible_propose_bi(partition):
+    """``grid_chain_sec11.py:132-145`` (host use; the device samples the same distribution)."""
+    fnode = random.choice(list(partition["b_nodes"]))
+    return partition.flip({fnode: -1 * partition.assignment[fnode]})
+
+
+def cut_accept(partition) -> bool:
+    """``grid_chain_sec11.py:171-179``."""
+    bound = 1
+    if partition.parent is not None:
+        bound = partition["base"] ** (-len(partition["cut_edges"]) + len(partition.parent["cut_edges"]))
+    return random.random() < bound
+
+
+def always_accept(partition) -> bool:
+    return True
+
+
+# ----------------------------------------------------------------------------------------
+# Partition
+# ----------------------------------------------------------------------------------------
+
+
+class Partition:
+    """``gerrychain.partition.Partition`` (host object: construction, ``flip``, lazy cached
+    updaters).  The device chain takes its graph, assignment and updaters from it."""
+
+    def __init__(self, graph=None, assignment=None, updaters=None, parent=None, flips=None):
+        if parent is None:
+            self.graph = graph
+            self.assignment = dict(assignment) if not isinstance(assignment, str) else \
+                {n: graph.nodes[n][assignment] for n in graph.nodes}
+            self.updaters = dict(updaters or {})
+            self.parent = None
+            self.flips = None
+        else:
+            self.graph = parent.graph
+            self.updaters = parent.updaters
+            self.parent = parent
+            self.flips = dict(flips)
+            self.assignment = dict(parent.assignment)
+            self.assignment.update(flips)
+        self._cache: Dict[str, Any] = {}
+        if "cut_edges" not in self.updaters:
+            self.updaters.setdefault("cut_edges", cut_edges)
+
+    @property
+    def parts(self):
+        out: Dict[Any, set] = {}
+        for n, p in self.assignment.items():
+            out.setdefault(p, set()).add(n)
+        return {p: frozenset(s) for p, s in out.items()}
+
+    def flip(self, flips):
+        return Partition(parent=self, flips=flips)
+
+    def __getitem__(self, key):
+        if key not in self._cache:
+            self._cache[key] = self.updaters[key](self)
+        return self._cache[key]
+
+    def __len__(self):
+        return len(set(self.assignment.values()))
+
+    def keys(self):
+        return self.updaters.keys()
+
+
+# ----------------------------------------------------------------------------------------
+# compile the reference's callables into device parameters
+# ----------------------------------------------------------------------------------------
+
+
+def _name(f) -> str:
+    return getattr(f, "__name__", type(f).__name__)
+
+
+@dataclass
+class ChainSpec:
+    spec: GraphSpec
+    labels: List[Any]
+    init: np.ndarray
+    base: float
+    pop_lo: int
+    pop_hi: int
+    pop_bounds_float: tuple
+    contig_first: bool = True
+    pop_key: str = "population"
+
+
+def compile_chain(proposal, constraints, accept, initial_state: Partition) -> ChainSpec:
+    """Map the reference's callables onto the device chain (NotImplementedError otherwise)."""
+    if _name(proposal) != "slow_reversible_propose_bi":
+        raise NotImplementedError(f"proposal {_name(proposal)!r}: the device implements "
+                                  "slow_reversible_propose_bi (grid_chain_sec11.py:132-145)")
+    cons = constraints.constraints if isinstance(constraints, Validator) else (
+        list(constraints) if isinstance(constraints, (list, tuple)) else [constraints])
+    contig_idx, bounds, pop_key = None, None, "population"
+    for i, c in enumerate(cons):
+        nm = _name(c)
+        if nm in ("single_flip_contiguous", "contiguous"):
+            contig_idx = i
+        elif isinstance(c, Bounds):
+            if bounds is not None:
+                raise NotImplementedError("only one population Bounds constraint is supported")
+            bounds = (i, c)
+            pop_key = getattr(c, "pop_key", "population")
+        else:
+            raise NotImplementedError(f"constraint {nm!r} is not implemented on the device")
+    if contig_idx is None:
+        raise NotImplementedError("the device chain always enforces single_flip_contiguous; include it")
+    an = _name(accept)
+    if an == "cut_accept":
+        if "base" not in initial_state.updaters:
+            raise ValueError("cut_accept reads partition['base']: add the 'base' updater")
+        base = float(initial_state["base"])
+    elif an == "always_accept":
+        base = 1.0
+    else:
+        raise NotImplementedError(f"accept {an!r}: the device implements cut_accept / always_accept")
+    g = initial_state.graph
+    labels = sorted(set(initial_state.assignment.values()))
+    if len(labels) != 2 or sorted(labels) != [-1, 1]:
+        raise NotImplementedError("slow_reversible_propose_bi flips -1 <-> 1: the plan must use labels -1 / 1")
+    for n in g.nodes:
+        g.nodes[n].setdefault(pop_key, 1)
+    spec = from_networkx(g, pop_attr=pop_key,
+                         pos={n: (g.nodes[n]["pos"] if "pos" in g.nodes[n] else n) for n in g.nodes}
+                         if all(isinstance(n, tuple) and len(n) == 2 for n in g.nodes) else None)
+    init = spec.assignment_array(initial_state.assignment, labels)
+    if bounds is not None:
+        lo_f, hi_f = bounds[1].bounds
+        lo, hi = int(math.ceil(lo_f)), int(math.floor(hi_f))
+        contig_first = contig_idx < bounds[0]
+    else:
+        lo_f, hi_f, lo, hi, contig_first = -math.inf, math.inf, -(2 ** 31), 2 ** 31 - 1, True
+    return ChainSpec(spec=spec, labels=labels, init=init, base=base, pop_lo=lo, pop_hi=hi,
+                     pop_bounds_float=(lo_f, hi_f), contig_first=contig_first, pop_key=pop_key)
+
+
+# ----------------------------------------------------------------------------------------
+# per-step views
+# ----------------------------------------------------------------------------------------
+
+
+class _AssignmentView(Mapping):
+    __slots__ = ("_a", "_spec", "_labels")
+
+    def __init__(self, a, spec, labels):
+        self._a, self._spec, self._labels = a, spec, labels
+
+    def __getitem__(self, node):
+        return self._labels[self._a[self._spec.index[node]]]
+
+    def __iter__(self):
+        return iter(self._spec.nodes)
+
+    def __len__(self):
+        return self._spec.n
+
+
+class StateView:
+    """A yielded chain state: ``part[key]`` for the reference's updaters, ``part.assignment``,
+    ``part.flips`` (stale on rejected steps, as in gerrychain), ``part.parent`` (None)."""
+
+    def __init__(self, chain, a: np.ndarray, flips, wait: int, cut: int, nb: int, step: int):
+        self._chain = chain
+        self._a = a
+        self.flips = flips
+        self.parent = None
+        self.graph = chain.initial_state.graph
+        self.updaters = chain.initial_state.updaters
+        self._cache: Dict[str, Any] = {"geom": wait}
+        self._cut, self._nb, self.step = cut, nb, step
+        self.assignment = _AssignmentView(a, chain.cspec.spec, chain.cspec.labels)
+
+    @property
+    def parts(self):
+        sp, lab = self._chain.cspec.spec, self._chain.cspec.labels
+        return {lab[d]: frozenset(sp.nodes[i] for i in np.nonzero(self._a == d)[0]) for d in range(len(lab))}
+
+    def __len__(self):
+        return len(self._chain.cspec.labels)
+
+    def __getitem__(self, key):
+        if key in self._cache:
+            return self._cache[key]
+        sp = self._chain.cspec.spec
+        if key == "cut_edges":
+            e = self._chain.edges
+            m = self._a[e[:, 0]] != self._a[e[:, 1]]
+            nodes = sp.nodes
+            val = {tuple(sorted((nodes[u], nodes[v]))) for u, v in e[m]}
+            assert len(val) == self._cut
+        elif key == "b_nodes" and self.updaters.get("b_nodes") is b_nodes_bi:
+            val = b_nodes_bi(self)
+        elif key == "population":
+            pops = np.bincount(self._a, weights=sp.pop, minlength=len(self._chain.cspec.labels))
+            val = {self._chain.cspec.labels[d]: int(pops[d]) for d in range(len(pops))}
+        else:
+            val = self.updaters[key](self)
+        self._cache[key] = val
+        return val
+
+
+class MarkovChain:
+    """``gerrychain.MarkovChain`` backed by the device (one chain, ``fc_run`` of size 1)."""
+
+    def __init__(self, proposal, constraints, accept, initial_state, total_steps: int, *,
+                 seed: int = 0, chain_id: int = 0, device: int = 0, chunk: int = 4096):
+        self.proposal, self.constraints, self.accept = proposal, constraints, accept
+        self.initial_state = initial_state
+        self.total_steps = int(total_steps)
+        self.seed, self.chain_id, self.device, self.chunk = seed, chain_id, device, chunk
+        self.cspec = compile_chain(proposal, constraints, accept, initial_state)
+        self.edges = self.cspec.spec.edges()
+        self._run = None
+        self._graph = None
+        # MarkovChain.__init__ validates the initial state [gc-0.2]
+        cons = constraints.constraints if isinstance(constraints, Validator) else (
+            list(constraints) if isinstance(constraints, (list, tuple)) else [constraints])
+        failed = [_name(c) for c in cons if not c(initial_state)]
+        if failed:
+            raise ValueError("The given initial_state is not valid according is_valid. "
+                             "The failed constraints were: " + ",".join(failed))
+
+    def __len__(self):
+        return self.total_steps
+
+    def _make_run(self, trace: bool, diag: int):
+        from .engine import FlipGraph, FlipRun, RunConfig
+        if self._graph is None:
+            self._graph = FlipGraph(self.cspec.spec)
+        cfg = RunConfig(seed=self.seed, chain_id_offset=self.chain_id, pop_lo=self.cspec.pop_lo,
+                        pop_hi=self.cspec.pop_hi, base=self.cspec.base, device=self.device, diag_mask=diag,
+                        trace_chains=1 if trace else 0, trace_cap=64 * self.chunk + 4096 if trace else 0,
+                        labels=tuple(self.cspec.labels))
+        return FlipRun(self._graph, self.cspec.init[None, :], cfg)
+
+    # ---- per-step iteration (debugging path) -------------------------------------------
+    def __iter__(self):
+        run = self._make_run(trace=True, diag=_lib.FC_DIAG_WAIT)
+        sp, lab = self.cspec.spec, self.cspec.labels
+        a = self.cspec.init.copy()
+        st = run.stats()
+        view = StateView(self, a.copy(), None, int(st["wait_cur"][0]), int(st["cut"][0]), int(st["nb"][0]), 0)
+        yield view
+        done = 1
+        while done < self.total_steps:
+            n = min(self.chunk, self.total_steps - done)
+            run.trace_reset()
+            run.steps(n)
+            for r in run.trace(0):
+                if not (r["flags"] & 1):
+                    continue
+                done += 1
+                if r["flags"] & 2:
+                    v = int(r["v"])
+                    a[v] = 1 - a[v]
+                    view = StateView(self, a.copy(), {sp.nodes[v]: lab[a[v]]}, int(r["wait"]), int(r["cut"]),
+                                     int(r["nb"]), done - 1)
+                yield view
+        run.close()
+
+    # ---- fast path -------------------------------------------------------------------
+    def run(self) -> "ChainResult":
+        """All ``total_steps`` yields on the device; the reference driver's outputs
+        (``grid_chain_sec11.py:366-419``) come back as a :class:`ChainResult`."""
+        diag = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
+        run = self._make_run(trace=False, diag=diag)
+        if self.total_steps > 1:
+            run.steps(self.total_steps - 1)
+        res = ChainResult.from_run(self, run, 0)
+        run.close()
+        return res
+
+
+@dataclass
+class ChainResult:
+    """What the reference's loop body + finalisation accumulate, for one chain."""
+
+    steps: int
+    proposals: int
+    accepted: int
+    waits_sum: int                      # wait.txt (:410-411)
+    rce_sum: int                        # sum of len(cut_edges) over yields
+    rbn_sum: int
+    cut_hist: np.ndarray                # counts of len(cut_edges) over yields
+    nb_hist: np.ndarray
+    cut_times: Dict[tuple, int]         # graph[u][v]["cut_times"]
+    num_flips: Dict[Hashable, int]      # graph.nodes[n]["num_flips"]
+    part_sum: Dict[Hashable, int]       # graph.nodes[n]["part_sum"] (finalised, :416-418)
+    last_flipped: Dict[Hashable, int]
+    lognum_flips: Dict[Hashable, float]
+    final_assignment: Dict[Hashable, Any]
+    stats: Dict[str, int] = field(default_factory=dict)
+
+    @classmethod
+    def from_run(cls, chain: MarkovChain, run, c: int) -> "ChainResult":
+        sp, lab = chain.cspec.spec, chain.cspec.labels
+        st = run.stats()
+        ch, nh = run.hist()
+        ct = run.cut_times()[c]
+        nf, ps, lf = run.flips()
+        fin = run.state()[c]
+        e = chain.edges
+        return cls(
+            steps=int(st["steps"][c]), proposals=int(st["proposals"][c]), accepted=int(st["accepted"][c]),
+            waits_sum=int(st["sum_wait"][c]), rce_sum=int(st["sum_cut"][c]), rbn_sum=int(st["sum_nb"][c]),
+            cut_hist=ch[c], nb_hist=nh[c],
+            cut_times={(sp.nodes[u], sp.nodes[v]): int(ct[i]) for i, (u, v) in enumerate(e)},
+            num_flips={sp.nodes[i]: int(nf[c, i]) for i in range(sp.n)},
+            part_sum={sp.nodes[i]: int(ps[c, i]) for i in range(sp.n)},
+            last_flipped={sp.nodes[i]: int(lf[c, i]) for i in range(sp.n)},
+            lognum_flips={sp.nodes[i]: math.log(int(nf[c, i]) + 1) for i in range(sp.n)},
+            final_assignment={sp.nodes[i]: lab[fin[i]] for i in range(sp.n)},
+            stats={k: int(v[c]) for k, v in st.items()})

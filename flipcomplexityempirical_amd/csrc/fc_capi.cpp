@@ -523,6 +523,16 @@ int fc_run_read_trace(fc_run *r, int32_t chain, fc_record *out, int64_t cap, int
     return FC_OK;
 }
 
+int fc_run_trace_reset(fc_run *r) {
+    if (!r) return fail(FC_ERR_ARG, "fc_run_trace_reset: null run");
+    if (int rc = fc_run_sync(r)) return rc;
+    std::vector<fc::ChainScalars> sc(r->n_chains);
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    for (auto &s : sc) s.trace_len = 0;
+    HIP_TRY(hipMemcpy(r->d_sc, sc.data(), sc.size() * sizeof(sc[0]), hipMemcpyHostToDevice));
+    return FC_OK;
+}
+
 int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist) {
     if (!r || !cut_hist || !nb_hist) return fail(FC_ERR_ARG, "fc_run_read_hist: null argument");
     if (!r->d_cut_hist) return fail(FC_ERR_ARG, "fc_run_read_hist: FC_DIAG_HIST not enabled");

@@ -188,6 +188,9 @@ class FlipRun:
             raise OverflowError(f"trace capacity {cap} exceeded ({n.value} records)")
         return out[:n.value]
 
+    def trace_reset(self):
+        check(_lib.load().fc_run_trace_reset(self.handle), "fc_run_trace_reset")
+
     def hist(self):
         E, n = self.graph.n_edges, self.graph.n
         ch = np.zeros((self.n_chains, E + 1), dtype=np.int64)

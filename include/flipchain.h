@@ -153,6 +153,8 @@ int fc_run_timings(fc_run *r, float *ms, int32_t cap, int32_t *n);
 int fc_run_read_stats(fc_run *r, fc_chain_stats *out);
 int fc_run_read_state(fc_run *r, int8_t *assign_out);
 int fc_run_read_trace(fc_run *r, int32_t chain, fc_record *out, int64_t cap, int64_t *len);
+/* Restart every traced chain's record buffer at 0 (chunked per-step iteration). */
+int fc_run_trace_reset(fc_run *r);
 int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist);      /* [c*(E+1)], [c*(n+1)] */
 int fc_run_read_edges(fc_run *r, int64_t *cut_times);                     /* [c*E], finalised     */
 /* num_flips / part_sum / last_flipped [c*n], finalised as grid_chain_sec11.py:416-418. */

@@ -1,0 +1,66 @@
+"""The two oracle restatements (plain C, gerrychain-0.2-faithful Python) agree bit-exactly,
+and the canonical stream matches the Random123 Philox known answers."""
+import numpy as np
+import pytest
+
+from flipcomplexityempirical_amd import graphs as G
+
+
+def test_philox_known_answers(cref):
+    from oracle.flipref import philox4x32_10
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, exp in kat:
+        assert tuple(cref.philox(ctr, key)) == exp
+        assert tuple(int(x) for x in philox4x32_10(*ctr, *key)) == exp
+
+
+@pytest.mark.parametrize("base,al", [(0.1, 0), (1.0, 2), (G.SEC11_MU, 1), (10, 0)])
+def test_c_oracle_equals_gc_faithful(cref, sec11, base, al):
+    from oracle.flipref import GcFaithfulChain
+    l1 = G.log1mp_table(sec11.n, 2)
+    plan = G.sec11_plan(al, sec11.nodes)
+    a0 = sec11.assignment_array(plan, [-1, 1])
+    (lo, hi), (ilo, ihi) = G.population_bounds(sec11.n, 2, 0.1)
+    gc = GcFaithfulChain(sec11, plan, base=base, pop_bounds=(lo, hi), seed=3, chain_id=al, log1mp=l1).run(250)
+    r = cref.run(sec11, a0, base=base, pop_lo=ilo, pop_hi=ihi, seed=3, chain_id=al, n_steps=250, log1mp=l1,
+                 trace_cap=100000)
+    gtr = np.array(gc.trace, dtype=np.int64)
+    tr = r["trace"]
+    assert len(tr) == len(gtr)
+    for i, f in enumerate(["draw", "v", "flags", "cut", "nb", "wait"]):
+        assert np.array_equal(tr[f], gtr[:, i]), f
+    assert np.array_equal(gc.assignment_ids(), r["final"])
+    for k in ("steps", "proposals", "draws", "accepted", "inv_contig", "inv_pop", "sum_cut", "sum_nb", "sum_wait"):
+        assert gc.stats[k] == r["stats"][k], k
+
+
+def test_tape_and_philox_agree(cref, sec11):
+    from oracle.flipref import draw_tape
+    l1 = G.log1mp_table(sec11.n, 2)
+    a0 = sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1])
+    _, (lo, hi) = G.population_bounds(sec11.n, 2, 0.1)
+    tape = draw_tape(9, 4, 30000)
+    r1 = cref.run(sec11, a0, base=0.8, pop_lo=lo, pop_hi=hi, seed=9, chain_id=4, n_steps=2000, log1mp=l1,
+                  trace_cap=100000)
+    r2 = cref.run(sec11, a0, base=0.8, pop_lo=lo, pop_hi=hi, seed=9, chain_id=4, n_steps=2000, log1mp=l1,
+                  trace_cap=100000, tape=tape)
+    assert np.array_equal(r1["trace"], r2["trace"])
+    assert r1["stats"] == r2["stats"]
+
+
+def test_oracle_rejects_invalid_initial_state(cref, sec11):
+    a0 = sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1]).copy()
+    a0[sec11.index[(0, 5)]] = 1
+    with pytest.raises(ValueError):
+        cref.run(sec11, a0, base=1.0, pop_lo=0, pop_hi=10 ** 6, seed=0, chain_id=0, n_steps=1)
+
+
+def test_oracle_stuck_cap(cref, sec11):
+    a0 = sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1])
+    # population bound pinned at exactly 798/798 -> no proposal can ever be valid
+    r = cref.run(sec11, a0, base=1.0, pop_lo=798, pop_hi=798, seed=0, chain_id=0, n_steps=10, max_draws=5000)
+    assert r["rc"] == 1 and r["stats"]["stuck"] == 1 and r["stats"]["steps"] == 0
+    assert r["stats"]["inv_pop"] > 0

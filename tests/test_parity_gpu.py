@@ -139,3 +139,22 @@ def test_invalid_initial_state_raises(gpu, sec11):
     with pytest.raises(ValueError):
         FlipRun(fg, sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1])[None, :],
                 RunConfig(pop_lo=799, pop_hi=10 ** 6))
+
+
+def test_sharded_equals_unsharded(gpu, sec11):
+    """Chain g gives the same trajectory whichever GPU/shard runs it (global chain ids)."""
+    from flipcomplexityempirical_amd import distributed as D
+    n_total, world = 96, 3
+    inits, bases = _configs(sec11, G.sec11_plan, G.SEC11_BASES, n_total)
+    fg = FlipGraph(sec11)
+    _, (lo, hi) = G.population_bounds(sec11.n, 2, 0.1)
+    full = FlipRun(fg, inits, RunConfig(seed=5, pop_lo=lo, pop_hi=hi), bases=bases).steps(2000)
+    fs, fa = full.stats(), full.state()
+    for r in range(world):
+        off, cnt = D.shard(n_total, world, r)
+        part = FlipRun(fg, inits[off:off + cnt], RunConfig(seed=5, pop_lo=lo, pop_hi=hi, chain_id_offset=off),
+                       bases=bases[off:off + cnt]).steps(2000)
+        ps = part.stats()
+        for k in ("steps", "proposals", "draws", "accepted", "sum_cut", "sum_wait", "cut", "nb"):
+            assert np.array_equal(ps[k], fs[k][off:off + cnt]), k
+        assert np.array_equal(part.state(), fa[off:off + cnt])
