@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -225,7 +226,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     r->n_chains = n_chains;
     r->npad = (n + 15) & ~15;
     r->words = (n + 63) / 64;
-    r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + 3 * r->words * 8;
+    r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + 3 * r->words * 8 + 4 * 64 * 4;
     r->chain_lds_bytes = (r->chain_lds_bytes + 15) & ~15;
     if ((size_t)r->chain_lds_bytes * fc::kWavesPerBlock > 160 * 1024)
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: graph too large for the wave-per-chain LDS layout");
@@ -421,6 +422,10 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.trace_cap = r->p.trace_cap;
     k.tape = r->d_tape;
     k.tape_draws = r->tape_draws;
+    k.nsub = 1;
+    if (const char *e = std::getenv("FC_NSUB")) k.nsub = std::atoi(e);
+    k.hit_stop = 32;
+    if (const char *e = std::getenv("FC_HIT_STOP")) k.hit_stop = std::atoi(e);
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : r->stream;
     if (r->n_launch_events == r->launch_events.size()) {
         hipEvent_t a, b;
@@ -430,8 +435,14 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     }
     auto &evp = r->launch_events[r->n_launch_events];
     HIP_TRY(hipEventRecord(evp.first, s));
-    const int e = fc::launch_flip_k2(k, r->g.ring_max, s);
-    if (e != 0) return fail(FC_ERR_HIP, std::string("flip kernel launch: ") + hipGetErrorString((hipError_t)e));
+    // the kernel keeps per-launch step and per-lane counters in 32 bits: launch in chunks
+    constexpr int64_t kChunk = int64_t(1) << 24;
+    for (int64_t done = 0; done < n_steps; done += kChunk) {
+        k.n_steps = std::min(kChunk, n_steps - done);
+        if (max_draws <= 0) k.max_draws = 65536 * k.n_steps;
+        const int e = fc::launch_flip_k2(k, r->g.ring_max, s);
+        if (e != 0) return fail(FC_ERR_HIP, std::string("flip kernel launch: ") + hipGetErrorString((hipError_t)e));
+    }
     HIP_TRY(hipEventRecord(evp.second, s));
     r->ev0 = evp.first;
     r->ev1 = evp.second;

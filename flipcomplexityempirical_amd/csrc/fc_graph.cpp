@@ -291,6 +291,33 @@ std::string build_host_graph(int32_t n, const int32_t *row_ptr, const int32_t *c
         }
     }
 
+    // The device's conflict test relies on x in R(y) <=> y in R(x).  Neighbour entries are
+    // symmetric by construction; a diagonal entry without its mirror is dropped (its node
+    // then has a break and loses exactness).
+    for (int32_t v = 0; v < n; ++v) {
+        for (size_t j = 0; j < ring[v].size(); ++j) {
+            if (nbr[v] >> j & 1u) continue;
+            const int32_t x = ring[v][j];
+            if (std::find(ring[x].begin(), ring[x].end(), v) != ring[x].end()) continue;
+            const int32_t L = (int32_t)ring[v].size();
+            std::vector<int32_t> ent;
+            uint32_t nn = 0, ll = 0;
+            for (int32_t q = 0, o = 0; q < L; ++q) {
+                if (q == (int32_t)j) continue;
+                ent.push_back(ring[v][q]);
+                if (nbr[v] >> q & 1u) nn |= 1u << o;
+                // the step out of the dropped entry's predecessor is now a break
+                if ((link[v] >> q & 1u) && (q + 1) % L != (int32_t)j) ll |= 1u << o;
+                ++o;
+            }
+            ring[v] = ent;
+            nbr[v] = nn;
+            link[v] = ll;
+            exact[v] = 0;
+            --j;
+        }
+    }
+
     int32_t rmax = 0;
     for (int32_t v = 0; v < n; ++v) rmax = std::max<int32_t>(rmax, (int32_t)ring[v].size());
     g.ring_max = rmax <= 8 ? 8 : 16;

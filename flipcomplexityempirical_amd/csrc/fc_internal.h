@@ -99,6 +99,8 @@ struct KParams {
     int64_t trace_cap;
     const uint32_t *tape;       // replay tape or null
     int64_t tape_draws;
+    int32_t nsub;               // max draw rounds of 64 per batch (1, 2, 4, 8)
+    int32_t hit_stop;           // start another round only while fewer boundary hits than this
 };
 
 // Launch wrappers (fc_kernels.hip).  Return a hipError_t as int.

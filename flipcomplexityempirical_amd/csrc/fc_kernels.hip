@@ -1,22 +1,26 @@
 // Flip-walk kernels for gfx950 (MI355X).
 //
-// One chain per wavefront.  The chain's state (int8 district per node, uint8 count of
-// foreign neighbours per node, its acceptance-threshold table and BFS bitmaps) lives in
-// LDS; the graph (one 32/48-byte record per node: meta, population, packed int16 link ring)
-// is shared by all chains and read through L1/L2.
+// One chain per wavefront.  The chain's state lives in LDS: int8 district per node, uint8
+// count of foreign neighbours per node (so |B| and boundary membership are O(1)), its
+// acceptance-threshold table, BFS bitmaps and a 64-slot staging area.  The graph (one
+// 32/48-byte record per node: meta, population, degree, packed int16 link ring) is shared by
+// all chains and read through L1/L2.
 //
-// A wave advances its chain in batches of 64 consecutive draws, one per lane:
-//   1. every lane evaluates its draw against the current state -- node by an exact
-//      Lemire map of the Philox word, boundary membership, the local contiguity test on
-//      the link ring, the population bound and the Metropolis threshold;
-//   2. a wave-uniform commit loop walks the lanes in draw order exactly as the reference's
-//      MarkovChain.__next__ would ([gc-0.2], used grid_chain_sec11.py:340-342,366):
-//      invalid proposals are skipped, rejected valid ones are steps that re-yield the
-//      state, and each accepted one is applied (a[v], populations, cut, boundary count);
-//      lanes whose ring an applied flip touched are re-drawn in the next batch, so the
-//      trajectory is bit-identical to a one-draw-at-a-time chain;
-//   3. the per-yield driver diagnostics (grid_chain_sec11.py:366-402) are accumulated
-//      lane-parallel from the committed masks.
+// A wave advances its chain in batches:
+//   1a. up to NSUB rounds of 64 Philox draws map to nodes (exact Lemire); draws whose node is
+//       a boundary node (fcnt[v] > 0) are proposals and are packed, in draw order, into up
+//       to 64 slots; other draws are not proposals (rejection sampling of random.choice
+//       over b_nodes, grid_chain_sec11.py:143);
+//   1b. every slot lane evaluates its proposal against the current state: link-ring reads,
+//       contiguity by the planar run rule, population bound, delta-cut, Metropolis threshold;
+//   2.  a wave-uniform commit loop walks the slots in draw order as the reference's
+//       MarkovChain.__next__ would ([gc-0.2], used grid_chain_sec11.py:340-342,366): invalid
+//       proposals are skipped, rejected valid ones re-yield the state, an accepted one is
+//       applied; later slots whose ring holds the flipped node (and non-hit draws whose node
+//       just entered the boundary) are redrawn in the next batch, so the trajectory is the
+//       one-draw-at-a-time chain bit for bit;
+//   3.  the per-yield driver diagnostics (grid_chain_sec11.py:366-402) are accumulated
+//       lane-parallel from the per-lane status bits.
 #include <hip/hip_runtime.h>
 
 #include "fc_internal.h"
@@ -26,6 +30,10 @@ namespace fc {
 
 namespace {
 
+// LDS operations of one wave execute in order; the fence only stops the compiler moving
+// LDS accesses across it.  Full waits (wave_sync) are used where lanes hand data to each
+// other through atomics (BFS).
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
 __device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ uint64_t bits_below(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
@@ -33,12 +41,9 @@ __device__ __forceinline__ uint64_t lane_range(int lo, int hi) { return bits_bel
 
 __device__ __forceinline__ int rl32(int x, int lane) { return __builtin_amdgcn_readlane(x, lane); }
 __device__ __forceinline__ uint32_t rlu(uint32_t x, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)x, lane); }
-__device__ __forceinline__ uint64_t rl64(uint64_t x, int lane) {
-    return ((uint64_t)rlu((uint32_t)(x >> 32), lane) << 32) | rlu((uint32_t)x, lane);
-}
 
-__device__ __forceinline__ int kth_set_bit(uint64_t x, int64_t k) {  // k >= 1
-    for (int64_t i = 1; i < k; ++i) x &= x - 1;
+__device__ __forceinline__ int kth_set_bit(uint64_t x, int k) {  // k >= 1
+    for (int i = 1; i < k; ++i) x &= x - 1;
     return __builtin_ctzll(x);
 }
 
@@ -60,14 +65,13 @@ __device__ __forceinline__ bool one_run(uint32_t nbrA, uint32_t brk, uint32_t fu
         cur = nx;
         rest &= rest - 1u;
     }
-    // wrap interval [cur, L) U [0, first)
-    const uint32_t first = nbrA & (0u - nbrA);
+    const uint32_t first = nbrA & (0u - nbrA);  // wrap interval [cur, L) U [0, first)
     cnt += (brk & ((full & ~(cur - 1u)) | (first - 1u))) != 0u;
     return cnt <= 1;
 }
 
 // Wave-cooperative BFS over the old district with v removed: are all old-district
-// neighbours of v (targets) connected?  Bitmaps in LDS; frontier words owned by lanes.
+// neighbours of v (each lane < RMAX may hold one as its target) connected to `start`?
 template <int RMAX>
 __device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, uint64_t *vis, uint64_t *front,
                          uint64_t *nxt, int words, int lane, int vf, int A, int my_target, int start,
@@ -91,8 +95,7 @@ __device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, u
             while (bits) {
                 const int b = __builtin_ctzll(bits);
                 bits &= bits - 1;
-                const int u = i * 64 + b;
-                const NodeRec<RMAX> r = G[u];
+                const NodeRec<RMAX> r = G[i * 64 + b];
                 const uint32_t nbr = (uint32_t)(r.meta >> kMetaNbrShift) & 0xffffu;
 #pragma unroll
                 for (int j = 0; j < RMAX; ++j) {
@@ -120,15 +123,17 @@ __device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, u
     }
 }
 
-struct LaneDraw {
-    int v, av, pv, delta, nA;
-    uint32_t inA, nbrA, L, nbr;
-    bool okdraw, isprop, exact, gam, s_lin, s_cyc, acc;
-};
+// per-lane status bits of the slots of one batch
+constexpr uint32_t ST_VS = 1u;   // valid step
+constexpr uint32_t ST_AC = 2u;   // accepted
+constexpr uint32_t ST_IC = 4u;   // invalid: contiguity
+constexpr uint32_t ST_IP = 8u;   // invalid: population
+constexpr uint32_t ST_BD = 16u;  // contiguity resolved by BFS
+constexpr uint32_t ST_BR = 32u;  // ... and its result
 
 }  // namespace
 
-template <int RMAX>
+template <int RMAX, int NSUB>
 __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
@@ -145,6 +150,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
     uint64_t *vis = T + (2 * RMAX + 2);
     uint64_t *front = vis + p.words;
     uint64_t *nxt = front + p.words;
+    uint32_t *slot = (uint32_t *)(nxt + p.words);  // [4][64]: node, word1, word2, draw offset
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
     // ---- load the chain into LDS -------------------------------------------------------
@@ -159,9 +165,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
     }
     ChainScalars *scp = p.sc + c;
     uint64_t draw = scp->draw;
-    int64_t steps = scp->steps;
-    int64_t proposals = scp->proposals, accepted = scp->accepted;
-    int64_t inv_contig = scp->inv_contig, inv_pop = scp->inv_pop;
+    int64_t steps = scp->steps;  // index of the current yield
     int64_t bfs_calls = scp->bfs_calls, bfs_levels = scp->bfs_levels;
     int64_t trace_len = scp->trace_len;
     int cut = scp->cut, nb = scp->nb;
@@ -170,7 +174,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
     int64_t wait_cur = scp->wait_cur;
     int last_flip = scp->last_flip;
     int stuck = 0;
-    const int64_t target = steps + p.n_steps;
+    int rem = (int)p.n_steps;  // steps still to take in this launch (host: n_steps < 2^31)
     uint64_t draw_cap = draw + (uint64_t)p.max_draws;
     if (p.tape && draw_cap > (uint64_t)p.tape_draws) draw_cap = (uint64_t)p.tape_draws;
     const uint32_t chain_gid = p.chain_id_offset + (uint32_t)c;
@@ -178,143 +182,180 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
     const bool want_wait = (p.diag & FC_DIAG_WAIT) != 0;
     const bool trace_on = p.trace && c < p.trace_chains;
 
-    // per-lane partial sums over yields, reduced once at the end
+    // per-lane accumulators, reduced once per launch
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
+    uint32_t n_prop = 0, n_acc = 0, n_ic = 0, n_ip = 0;
     wave_sync();
 
-    while (steps < target) {
+    while (rem > 0) {
         if (draw >= draw_cap) {
             stuck = 1;
             break;
         }
-        const int avail = (int)((draw_cap - draw) < 64 ? (draw_cap - draw) : 64);
-        // ---- 1. speculative evaluation: lane = draw ----------------------------------
-        const uint64_t d = draw + (uint64_t)lane;
-        Words4 w;
-        if (p.tape) {
-            const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + (lane < avail ? d : draw)) * 6;
-            w = Words4{t[0], t[1], t[2], t[3]};
-        } else {
-            w = philox4x32_10((uint32_t)d, (uint32_t)(d >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
+        const uint64_t room = draw_cap - draw;
+        // ---- 1a. draws -> nodes; boundary hits packed, in draw order, into <= 64 slots ----
+        int nh = 0;       // boundary hits seen
+        int gen = 0;      // draws generated (offsets 0..gen-1 of this batch)
+        int rv[NSUB];     // node of this lane's draw in round r (offset 64 r + lane)
+        uint64_t nonhit[NSUB];
+#pragma unroll
+        for (int r = 0; r < NSUB; ++r) {
+            rv[r] = -1;
+            nonhit[r] = 0;
+            if ((r > 0 && nh >= p.hit_stop) || nh >= 64 || (uint64_t)gen >= room) continue;
+            const int off = gen + lane;
+            const bool inrange = (uint64_t)off < room;
+            const uint64_t dr = draw + (uint64_t)off;
+            Words4 w;
+            if (p.tape) {
+                const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + (inrange ? dr : draw)) * 6;
+                w = Words4{t[0], t[1], t[2], t[3]};
+            } else {
+                w = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
+            }
+            const uint64_t m = (uint64_t)w.x0 * (uint64_t)(uint32_t)n;
+            const int v = (int)(m >> 32);
+            const bool ok = inrange && (uint32_t)m >= p.lemire_thresh;
+            const bool hit = ok && fcnt[v] != 0;
+            const uint64_t hm = __ballot(hit);
+            const int pos = nh + __popcll(hm & bits_below(lane));
+            if (hit && pos < 64) {
+                slot[pos] = (uint32_t)v;
+                slot[64 + pos] = w.x1;
+                slot[128 + pos] = w.x2;
+                slot[192 + pos] = (uint32_t)off;
+            }
+            rv[r] = v;
+            uint64_t nm = __ballot(ok && !hit);
+            const int cnt = __popcll(hm);
+            if (nh + cnt > 64) {  // the 64th hit closes the batch inside this round
+                const int last = kth_set_bit(hm, 64 - nh);
+                gen += last + 1;
+                nm &= bits_below(last + 1);
+            } else {
+                gen = (uint64_t)(gen + 64) < room ? gen + 64 : (int)room;
+            }
+            nonhit[r] = nm;
+            nh += cnt;
         }
-        LaneDraw L;
-        const uint64_t m = (uint64_t)w.x0 * (uint64_t)(uint32_t)n;
-        L.v = (int)(m >> 32);
-        L.okdraw = ((uint32_t)m >= p.lemire_thresh) && lane < avail;
-        const NodeRec<RMAX> rec = G[L.v];
-        L.av = a[L.v];
-        L.pv = rec.pop;
-        L.L = (uint32_t)(rec.meta & kMetaLenMask);
-        const uint32_t full = (L.L >= 32) ? 0xffffffffu : ((1u << L.L) - 1u);
-        L.nbr = (uint32_t)(rec.meta >> kMetaNbrShift) & 0xffffu;
+        const int ns = nh < 64 ? nh : 64;
+        compiler_fence();
+
+        // ---- 1b. evaluate every slot against the current state ---------------------------
+        const bool has = lane < ns;
+        const int off_l = has ? (int)slot[192 + lane] : gen;
+        const uint64_t d = draw + (uint64_t)off_l;
+        const int v = has ? (int)slot[lane] : 0;
+        const uint32_t w1 = slot[64 + lane], w2 = slot[128 + lane];
+        const NodeRec<RMAX> rec = G[v];
+        const int av = a[v];
+        const int pv = rec.pop;
+        const uint32_t Ln = (uint32_t)(rec.meta & kMetaLenMask);
+        const uint32_t full = (1u << Ln) - 1u;
+        const uint32_t nbr = (uint32_t)(rec.meta >> kMetaNbrShift) & 0xffffu;
         const uint32_t link = (uint32_t)(rec.meta >> kMetaLinkShift) & 0xffffu;
         uint32_t inA = 0;
 #pragma unroll
-        for (int i = 0; i < RMAX; ++i) inA |= (uint32_t)(a[ring_entry<RMAX>(rec.ring, i)] == L.av) << i;
+        for (int i = 0; i < RMAX; ++i) inA |= (uint32_t)(a[ring_entry<RMAX>(rec.ring, i)] == av) << i;
         inA &= full;
-        L.inA = inA;
-        L.nbrA = inA & L.nbr;
-        L.nA = __popc(L.nbrA);
-        const int nBn = rec.deg - L.nA;
-        L.isprop = L.okdraw && nBn > 0;
+        const uint32_t nbrA = inA & nbr;
+        const int nA = __popc(nbrA);
+        const int nBn = rec.deg - nA;
+        const bool isprop = has && nBn > 0;
+        bool s_lin, s_cyc;
         {
-            const uint32_t rot = L.L ? (((inA >> 1) | (inA << (L.L - 1))) & full) : 0u;
+            const uint32_t rot = Ln ? (((inA >> 1) | (inA << (Ln - 1))) & full) : 0u;
             const uint32_t lk = inA & rot & link;
-            L.s_lin = one_run(L.nbrA, full & ~lk, full);
-            const uint32_t vlink = (L.L >= 2 && (inA & 1u) && ((inA >> (L.L - 1)) & 1u)) ? (1u << (L.L - 1)) : 0u;
-            L.s_cyc = one_run(L.nbrA, full & ~(lk | vlink), full);
+            s_lin = one_run(nbrA, full & ~lk, full);
+            const uint32_t vlink = (Ln >= 2 && (inA & 1u) && ((inA >> (Ln - 1)) & 1u)) ? (1u << (Ln - 1)) : 0u;
+            s_cyc = one_run(nbrA, full & ~(lk | vlink), full);
         }
-        L.exact = (rec.meta & kMetaExact) && !force_bfs;
-        L.gam = (rec.meta & kMetaGamma) != 0;
-        L.delta = L.nA - nBn;
-        L.acc = mant53(w.x1, w.x2) < T[L.delta + RMAX];
+        const bool exact = (rec.meta & kMetaExact) && !force_bfs;
+        const bool gam = (rec.meta & kMetaGamma) != 0;
+        const int delta = nA - nBn;
+        const bool acc = mant53(w1, w2) < T[delta + RMAX];
+        // packed for the wave-uniform apply: node | A | outer | delta+16 | nA
+        const uint32_t pk = (uint32_t)v | ((uint32_t)av << 15) | ((uint32_t)gam << 16) |
+                            ((uint32_t)(delta + 16) << 17) | ((uint32_t)nA << 22);
+        const uint32_t pk2 = inA | (nbr << 16);
 
-        // ---- 2. commit loop (wave-uniform) -------------------------------------------
-        const uint64_t P = __ballot(L.isprop);
-        const uint64_t ACC = __ballot(L.acc);
-        uint64_t BFSDONE = 0, BFSRES = 0, ACCM = 0, VSM = 0, INVC = 0, INVP = 0;
-        int end = avail, pos = 0;
-        const int cut0 = cut, nb0 = nb;
+        // ---- 2. commit loop (wave-uniform) -----------------------------------------------
+        uint32_t st = 0;
+        int end = ns, pos = 0;
+        int trunc_off = gen;  // first draw offset not consumed by this batch
+        bool target_hit = false;
+        const int cut0 = cut, nb0 = nb, rem0 = rem;
         const int64_t steps0 = steps;
         const int last_flip0 = last_flip;
         const int a_last0 = last_flip0 >= 0 ? (int)a[last_flip0] : 0;
-        int cut_after = cut, nb_after = nb;
+        int cut_after = 0, nb_after = 0;
         while (pos < end) {
-            // per-lane status against the current populations / outer-face counts
-            const bool bdone = (BFSDONE >> lane) & 1ull;
-            const int other = 1 - L.av;
-            const bool touch = (other == 0 ? ng0 : ng1) > 0;
-            bool known, ok;
-            if (L.nA == 0) {
-                known = true;
+            bool known = true, ok;
+            if (st & ST_BD) {
+                ok = (st & ST_BR) != 0;
+            } else if (nA == 0) {
                 ok = false;
-            } else if (bdone) {
-                known = true;
-                ok = (BFSRES >> lane) & 1ull;
-            } else if (L.exact) {
-                known = true;
-                ok = (L.gam && !touch) ? L.s_cyc : L.s_lin;
+            } else if (exact) {
+                const bool touch = (av ? ng0 : ng1) > 0;  // the other district touches the outer face
+                ok = (gam && !touch) ? s_cyc : s_lin;
             } else {
-                known = L.s_lin;
-                ok = L.s_lin;
+                known = s_lin;
+                ok = s_lin;
             }
-            const int pa = L.av == 0 ? pops0 : pops1, pb = L.av == 0 ? pops1 : pops0;
-            const bool popok = (pa - L.pv >= p.pop_lo) && (pb + L.pv <= p.pop_hi);
-            const uint64_t VAL = __ballot(L.isprop && known && ok && popok);
-            const uint64_t UNK = __ballot(L.isprop && !known);
-            const uint64_t IC = __ballot(L.isprop && known && !ok);
-            const uint64_t IP = __ballot(L.isprop && known && ok && !popok);
-            const uint64_t ev = ((VAL & ACC) | UNK) & lane_range(pos, end);
-            const int f = ev ? __builtin_ctzll(ev) : end;
-            const uint64_t seg = lane_range(pos, f);
-            const int nvalid = __popcll(VAL & seg);
-            if (steps + nvalid >= target) {
-                const int e = kth_set_bit(VAL & seg, target - steps);
-                const uint64_t s2 = lane_range(pos, e + 1);
-                VSM |= VAL & s2;
-                INVC |= IC & s2;
-                INVP |= IP & s2;
-                steps = target;
+            const int pa = av ? pops1 : pops0, pb = av ? pops0 : pops1;
+            const bool popok = (pa - pv >= p.pop_lo) && (pb + pv <= p.pop_hi);
+            const bool prop = isprop && lane >= pos && lane < end;
+            const bool valid = prop && known && ok && popok;
+            const uint64_t VAL = __ballot(valid);
+            const uint64_t EV = __ballot((valid && acc) || (prop && !known));
+            const int f = EV ? __builtin_ctzll(EV) : end;
+            const uint64_t segv = VAL & bits_below(f);
+            const int nvalid = __popcll(segv);
+            const uint32_t bits = valid ? ST_VS : (ok ? ST_IP : ST_IC);
+            if (nvalid >= rem) {  // the launch's last step lies in this segment
+                const int e = kth_set_bit(segv, rem);
+                if (prop && lane <= e) st |= bits;
+                rem = 0;
                 end = e + 1;
+                target_hit = true;
                 break;
             }
-            VSM |= VAL & seg;
-            INVC |= IC & seg;
-            INVP |= IP & seg;
-            steps += nvalid;
+            if (prop && lane < f) st |= bits;
+            rem -= nvalid;
             pos = f;
             if (f >= end) break;
-            if ((UNK >> f) & 1ull) {
-                // resolve lane f by device BFS on the current state
-                const int vf = rl32(L.v, f), Af = rl32(L.av, f);
-                const uint32_t nbrAf = rlu(L.nbrA, f);
+            if (!((VAL >> f) & 1ull)) {
+                // undecided contiguity at slot f: device BFS on the current state
+                const uint32_t pkf = rlu(pk, f), nbrAf = rlu(pk2, f) & rlu(pk2, f) >> 16;
                 int my_target = -1, start = -1;
 #pragma unroll
                 for (int k2 = 0; k2 < RMAX / 2; ++k2) {
                     const uint32_t wrd = rlu(rec.ring[k2], f);
                     if ((lane >> 1) == k2) my_target = (int)((wrd >> (16 * (lane & 1))) & 0xffffu);
-                    const int j0 = 2 * k2, j1 = 2 * k2 + 1;
-                    if (start < 0 && ((nbrAf >> j0) & 1u)) start = (int)(wrd & 0xffffu);
-                    if (start < 0 && ((nbrAf >> j1) & 1u)) start = (int)(wrd >> 16);
+                    if (start < 0 && ((nbrAf >> (2 * k2)) & 1u)) start = (int)(wrd & 0xffffu);
+                    if (start < 0 && ((nbrAf >> (2 * k2 + 1)) & 1u)) start = (int)(wrd >> 16);
                 }
                 if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
-                const bool res = wave_bfs<RMAX>(G, a, vis, front, nxt, p.words, lane, vf, Af, my_target, start, bfs_levels);
+                const bool res = wave_bfs<RMAX>(G, a, vis, front, nxt, p.words, lane, (int)(pkf & 0x7fffu),
+                                                (int)((pkf >> 15) & 1u), my_target, start, bfs_levels);
                 ++bfs_calls;
-                BFSDONE |= 1ull << f;
-                if (res) BFSRES |= 1ull << f;
+                if (lane == f) st |= ST_BD | (res ? ST_BR : 0u);
                 continue;
             }
-            // ---- accept lane f: apply the flip ---------------------------------------
-            const int vf = rl32(L.v, f), Af = rl32(L.av, f), pvf = rl32(L.pv, f);
-            const int df = rl32(L.delta, f), nAf = rl32(L.nA, f);
-            const uint32_t inAf = rlu(L.inA, f), nbrf = rlu(L.nbr, f);
-            const bool gamf = rl32((int)L.gam, f) != 0;
-            int my_e = -1;
+            // ---- accept slot f: apply the flip -----------------------------------------
+            const uint32_t pkf = rlu(pk, f), pk2f = rlu(pk2, f);
+            const int vf = (int)(pkf & 0x7fffu), Af = (int)((pkf >> 15) & 1u);
+            const bool gamf = (pkf >> 16) & 1u;
+            const int df = (int)((pkf >> 17) & 31u) - 16, nAf = (int)((pkf >> 22) & 31u);
+            const int pvf = rl32(pv, f);
+            const uint32_t inAf = pk2f & 0xffffu, nbrf = pk2f >> 16;
+            uint32_t rw[RMAX / 2];
 #pragma unroll
-            for (int k2 = 0; k2 < RMAX / 2; ++k2) {
-                const uint32_t wrd = rlu(rec.ring[k2], f);
-                if ((lane >> 1) == k2) my_e = (int)((wrd >> (16 * (lane & 1))) & 0xffffu);
-            }
+            for (int k2 = 0; k2 < RMAX / 2; ++k2) rw[k2] = rlu(rec.ring[k2], f);
+            uint32_t sel = rw[0];
+#pragma unroll
+            for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((lane >> 1) == k2) ? rw[k2] : sel;
+            const int my_e = (int)((sel >> (16 * (lane & 1))) & 0xffffu);
             const bool is_nbr = lane < RMAX && ((nbrf >> lane) & 1u);
             const bool inA_l = (inAf >> lane) & 1u;
             bool enter = false, leave = false;
@@ -324,7 +365,8 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
                 enter = inA_l && old == 0;
                 leave = !inA_l && old == 1;
             }
-            const int dnb = __popcll(__ballot(enter)) - __popcll(__ballot(leave));
+            uint64_t ent = __ballot(enter);
+            const int dnb = __popcll(ent) - __popcll(__ballot(leave));
             if (lane == 0) {
                 a[vf] = (int8_t)(1 - Af);
                 fcnt[vf] = (uint8_t)nAf;
@@ -333,38 +375,69 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
             if (gamf) { if (Af == 0) { --ng0; ++ng1; } else { --ng1; ++ng0; } }
             cut += df;
             nb += dnb;
-            ++steps;
-            VSM |= 1ull << f;
-            ACCM |= 1ull << f;
+            --rem;
             last_flip = vf;
-            if (lane == f) { cut_after = cut; nb_after = nb; }
-            wave_sync();
-            // lanes whose ring contains vf were evaluated on a stale neighbourhood
-            bool hit = false;
-            if (L.okdraw && lane > f) {
-                hit = L.v == vf;
+            if (lane == f) {
+                st |= ST_VS | ST_AC;
+                cut_after = cut;
+                nb_after = nb;
+            }
+            // slots after f whose node lies in R(vf) + {vf} (rings are symmetric) saw a stale
+            // neighbourhood
+            bool hit = v == vf;
 #pragma unroll
-                for (int i = 0; i < RMAX; ++i) hit |= ring_entry<RMAX>(rec.ring, i) == vf;
+            for (int i = 0; i < RMAX; ++i) hit |= v == (int)((rw[i >> 1] >> (16 * (i & 1))) & 0xffffu);
+            const uint64_t aff = __ballot(hit && lane > f && lane < end);
+            if (aff) end = __builtin_ctzll(aff);
+            // non-hit draws after f whose node just entered the boundary would now propose
+            if (ent) {
+                const int off_f = rl32(off_l, f);
+                int t_na = trunc_off;
+                while (ent) {
+                    const int u = rl32(my_e, __builtin_ctzll(ent));
+                    ent &= ent - 1;
+#pragma unroll
+                    for (int r = 0; r < NSUB; ++r) {
+                        const uint64_t m2 = __ballot(((nonhit[r] >> lane) & 1ull) && rv[r] == u && 64 * r + lane > off_f);
+                        if (m2) {
+                            const int t = 64 * r + __builtin_ctzll(m2);
+                            if (t < t_na) t_na = t;
+                        }
+                    }
+                }
+                if (t_na < trunc_off) {
+                    trunc_off = t_na;
+                    const int e2 = __popcll(__ballot(has && off_l < t_na));
+                    if (e2 < end) end = e2;
+                }
             }
-            const uint64_t aff = __ballot(hit);
-            if (aff) {
-                const int fa = __builtin_ctzll(aff);
-                if (fa < end) end = fa;
-            }
+            compiler_fence();
             pos = f + 1;
-            if (steps >= target) {
+            if (rem == 0) {
                 end = pos;
+                target_hit = true;
                 break;
             }
         }
+        // draws consumed by the committed slots [0, end)
+        int consumed;
+        if (target_hit) {
+            consumed = rl32(off_l, end - 1) + 1;
+        } else {
+            consumed = end < ns ? rl32(off_l, end) : gen;
+            if (trunc_off < consumed) consumed = trunc_off;
+        }
+        steps = steps0 + (rem0 - rem);
 
-        // ---- 3. lane-parallel bookkeeping of the committed batch ------------------------
-        const uint64_t done_mask = bits_below(end);
-        proposals += __popcll(P & done_mask);
-        accepted += __popcll(ACCM);
-        inv_contig += __popcll(INVC);
-        inv_pop += __popcll(INVP);
-        const bool is_acc = (ACCM >> lane) & 1ull;
+        // ---- 3. lane-parallel bookkeeping of the committed batch ----------------------------
+        const bool done = lane < end;
+        const bool is_acc = (st & ST_AC) != 0;
+        n_prop += (isprop && done) ? 1u : 0u;
+        n_acc += is_acc ? 1u : 0u;
+        n_ic += (st & ST_IC) ? 1u : 0u;
+        n_ip += (st & ST_IP) ? 1u : 0u;
+        const uint64_t ACCM = __ballot(is_acc);
+        const uint64_t VSM = __ballot((st & ST_VS) != 0);
         const uint64_t later_acc = ACCM & ~bits_below(lane + 1);
         const int next_acc = later_acc ? __builtin_ctzll(later_acc) : end;
         const int run_len = is_acc ? 1 + __popcll(VSM & lane_range(lane + 1, next_acc)) : 0;
@@ -396,75 +469,74 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
             acc_nb2 += (int64_t)nb0 * nb0 * r0;
             acc_wait += wait_cur * r0;
         }
-        const int t_acc = (int)(steps0 + __popcll(VSM & bits_below(lane + 1)));  // yield index of this lane
-        if (p.diag & FC_DIAG_HIST) {
-            if (is_acc) {
-                atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
-                atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb_after], (unsigned long long)run_len);
+        if (p.diag & (FC_DIAG_HIST | FC_DIAG_FLIPS | FC_DIAG_EDGES)) {
+            const int64_t t_acc = steps0 + __popcll(VSM & bits_below(lane + 1));  // yield index of this slot
+            if (p.diag & FC_DIAG_HIST) {
+                if (is_acc) {
+                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
+                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb_after], (unsigned long long)run_len);
+                }
+                if (lane == 0 && r0) {
+                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut0], (unsigned long long)r0);
+                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb0], (unsigned long long)r0);
+                }
             }
-            if (lane == 0 && r0) {
-                atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut0], (unsigned long long)r0);
-                atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb0], (unsigned long long)r0);
+            if (p.diag & FC_DIAG_FLIPS) {
+                // part.flips is stale on rejected steps: every yield of a run repeats the update
+                // for the node whose flip created the state (grid_chain_sec11.py:396-400).
+                int64_t *nf = p.num_flips + (size_t)c * n, *ps = p.part_sum + (size_t)c * n;
+                unsigned long long *lf = (unsigned long long *)(p.last_flipped + (size_t)c * n);
+                if (lane == 0 && r0 && last_flip0 >= 0) {
+                    const int64_t t_last = steps0 + r0;
+                    const int64_t old = (int64_t)atomicExch(lf + last_flip0, (unsigned long long)t_last);
+                    atomicAdd((unsigned long long *)(ps + last_flip0), (unsigned long long)(-(int64_t)p.labels[a_last0] * (t_last - old)));
+                    atomicAdd((unsigned long long *)(nf + last_flip0), (unsigned long long)r0);
+                }
+                __builtin_amdgcn_s_waitcnt(0);
+                if (is_acc) {
+                    const int64_t t_last = t_acc + run_len - 1;
+                    const int64_t old = (int64_t)atomicExch(lf + v, (unsigned long long)t_last);
+                    atomicAdd((unsigned long long *)(ps + v), (unsigned long long)(-(int64_t)p.labels[1 - av] * (t_last - old)));
+                    atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
+                }
             }
-        }
-        if (p.diag & FC_DIAG_FLIPS) {
-            // part.flips is stale on rejected steps: every yield of a run repeats the update
-            // for the node whose flip created the state (grid_chain_sec11.py:396-400).
-            int64_t *nf = p.num_flips + (size_t)c * n, *ps = p.part_sum + (size_t)c * n;
-            unsigned long long *lf = (unsigned long long *)(p.last_flipped + (size_t)c * n);
-            if (lane == 0 && r0 && last_flip0 >= 0) {
-                const int64_t t_last = steps0 + r0;
-                const int64_t old = (int64_t)atomicExch(lf + last_flip0, (unsigned long long)t_last);
-                atomicAdd((unsigned long long *)(ps + last_flip0), (unsigned long long)(-(int64_t)p.labels[a_last0] * (t_last - old)));
-                atomicAdd((unsigned long long *)(nf + last_flip0), (unsigned long long)r0);
-            }
-            __builtin_amdgcn_s_waitcnt(0);
-            if (is_acc) {
-                const int64_t t_last = (int64_t)t_acc + run_len - 1;
-                const int64_t old = (int64_t)atomicExch(lf + L.v, (unsigned long long)t_last);
-                atomicAdd((unsigned long long *)(ps + L.v), (unsigned long long)(-(int64_t)p.labels[1 - L.av] * (t_last - old)));
-                atomicAdd((unsigned long long *)(nf + L.v), (unsigned long long)run_len);
-            }
-        }
-        if ((p.diag & FC_DIAG_EDGES) && is_acc) {
-            int64_t *ea = p.edge_acc + (size_t)c * p.n_edges;
-            unsigned long long *es = (unsigned long long *)(p.edge_since + (size_t)c * p.n_edges);
-            for (int i = 0; i < RMAX; ++i) {
-                if (!((L.nbr >> i) & 1u)) continue;
-                const int e = p.ring_eid[(size_t)L.v * RMAX + i];
-                if ((L.inA >> i) & 1u) {
-                    atomicExch(es + e, (unsigned long long)t_acc);             // becomes cut
-                } else {
-                    const int64_t since = (int64_t)atomicAdd(es + e, 0ull);    // becomes uncut
-                    atomicAdd((unsigned long long *)(ea + e), (unsigned long long)((int64_t)t_acc - since));
+            if ((p.diag & FC_DIAG_EDGES) && is_acc) {
+                int64_t *ea = p.edge_acc + (size_t)c * p.n_edges;
+                unsigned long long *es = (unsigned long long *)(p.edge_since + (size_t)c * p.n_edges);
+                for (int i = 0; i < RMAX; ++i) {
+                    if (!((nbr >> i) & 1u)) continue;
+                    const int e = p.ring_eid[(size_t)v * RMAX + i];
+                    if ((inA >> i) & 1u) {
+                        atomicExch(es + e, (unsigned long long)t_acc);             // becomes cut
+                    } else {
+                        const int64_t since = (int64_t)atomicAdd(es + e, 0ull);    // becomes uncut
+                        atomicAdd((unsigned long long *)(ea + e), (unsigned long long)(t_acc - since));
+                    }
                 }
             }
         }
         if (trace_on) {
-            const bool in_done = lane < end && L.isprop;
+            const uint64_t P = __ballot(isprop && done);
             const uint64_t mine = ACCM & bits_below(lane + 1);
             const int src = mine ? 63 - __builtin_clzll(mine) : 0;
             const int c_j = __shfl(cut_after, src), n_j = __shfl(nb_after, src);
             const long long w_j = __shfl((long long)my_wait, src);
-            const int64_t idx = trace_len + __popcll(P & done_mask & bits_below(lane));
-            if (in_done && idx < p.trace_cap) {
+            const int64_t idx = trace_len + __popcll(P & bits_below(lane));
+            if (isprop && done && idx < p.trace_cap) {
                 fc_record &rr = p.trace[(size_t)c * p.trace_cap + idx];
-                const bool valid = (VSM >> lane) & 1ull;
+                const bool valid = (st & ST_VS) != 0;
                 rr.draw = (int64_t)d;
-                rr.v = L.v;
-                rr.flags = valid ? (1 | (is_acc ? 2 : 0)) : (((INVC >> lane) & 1ull) ? 4 : 8);
+                rr.v = v;
+                rr.flags = valid ? (1 | (is_acc ? 2 : 0)) : ((st & ST_IC) ? 4 : 8);
                 rr.cut = mine ? c_j : cut0;
                 rr.nb = mine ? n_j : nb0;
                 rr.wait = valid ? (mine ? (int64_t)w_j : wait_cur) : 0;
             }
-            trace_len += __popcll(P & done_mask);
+            trace_len += __popcll(P);
         }
-        if (ACCM) {
-            const int la = 63 - __builtin_clzll(ACCM);
-            wait_cur = (int64_t)__shfl((long long)my_wait, la);
-        }
-        draw += (uint64_t)end;
-        wave_sync();
+        if (ACCM) wait_cur = (int64_t)__shfl((long long)my_wait, 63 - __builtin_clzll(ACCM));
+        draw += (uint64_t)consumed;
+        compiler_fence();
     }
 
     // ---- write back ---------------------------------------------------------------------
@@ -476,6 +548,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
             gf[i] = ((const uint4 *)fcnt)[i];
         }
     }
+    int64_t cnt_prop = n_prop, cnt_acc = n_acc, cnt_ic = n_ic, cnt_ip = n_ip;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         acc_cut += __shfl_xor((long long)acc_cut, off);
@@ -483,14 +556,18 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
         acc_wait += __shfl_xor((long long)acc_wait, off);
         acc_cut2 += __shfl_xor((long long)acc_cut2, off);
         acc_nb2 += __shfl_xor((long long)acc_nb2, off);
+        cnt_prop += __shfl_xor((long long)cnt_prop, off);
+        cnt_acc += __shfl_xor((long long)cnt_acc, off);
+        cnt_ic += __shfl_xor((long long)cnt_ic, off);
+        cnt_ip += __shfl_xor((long long)cnt_ip, off);
     }
     if (lane == 0) {
         scp->draw = draw;
         scp->steps = steps;
-        scp->proposals = proposals;
-        scp->accepted = accepted;
-        scp->inv_contig = inv_contig;
-        scp->inv_pop = inv_pop;
+        scp->proposals += cnt_prop;
+        scp->accepted += cnt_acc;
+        scp->inv_contig += cnt_ic;
+        scp->inv_pop += cnt_ip;
         scp->bfs_calls = bfs_calls;
         scp->bfs_levels = bfs_levels;
         scp->trace_len = trace_len;
@@ -515,12 +592,26 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream) {
     const int blocks = (p.n_chains + kWavesPerBlock - 1) / kWavesPerBlock;
     const size_t lds = (size_t)p.chain_lds_bytes * kWavesPerBlock;
     hipStream_t s = (hipStream_t)stream;
-    if (ring_max == 8)
-        hipLaunchKernelGGL(flip_k2_kernel<8>, dim3(blocks), dim3(kWave * kWavesPerBlock), lds, s, p);
-    else if (ring_max == 16)
-        hipLaunchKernelGGL(flip_k2_kernel<16>, dim3(blocks), dim3(kWave * kWavesPerBlock), lds, s, p);
-    else
+    const dim3 grid(blocks), block(kWave * kWavesPerBlock);
+#define FC_LAUNCH(R, S) hipLaunchKernelGGL((flip_k2_kernel<R, S>), grid, block, lds, s, p)
+    if (ring_max == 8) {
+        switch (p.nsub) {
+            case 1: FC_LAUNCH(8, 1); break;
+            case 2: FC_LAUNCH(8, 2); break;
+            case 4: FC_LAUNCH(8, 4); break;
+            default: return (int)hipErrorInvalidValue;
+        }
+    } else if (ring_max == 16) {
+        switch (p.nsub) {
+            case 1: FC_LAUNCH(16, 1); break;
+            case 2: FC_LAUNCH(16, 2); break;
+            case 4: FC_LAUNCH(16, 4); break;
+            default: return (int)hipErrorInvalidValue;
+        }
+    } else {
         return (int)hipErrorInvalidValue;
+    }
+#undef FC_LAUNCH
     return (int)hipGetLastError();
 }
 

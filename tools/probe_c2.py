@@ -1,4 +1,4 @@
-"""Quick C2 throughput probe (4096 chains, sec11, base sweep)."""
+"""C2 throughput probe: python tools/probe_c2.py [chains] [steps/launch] [base_index|-1] [iters]"""
 import sys, time, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -7,18 +7,17 @@ from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
 spec = G.sec11_graph(); fg = FlipGraph(spec)
 C = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
+B = int(sys.argv[3]) if len(sys.argv) > 3 else -1
+IT = int(sys.argv[4]) if len(sys.argv) > 4 else 6
 plans = [spec.assignment_array(G.sec11_plan(al, spec.nodes), [-1, 1]) for al in range(3)]
 inits = np.stack([plans[(c // 10) % 3] for c in range(C)])
-bases = np.asarray([G.SEC11_BASES[c % 10] for c in range(C)])
+bases = np.asarray([G.SEC11_BASES[c % 10 if B < 0 else B] for c in range(C)])
 (_, _), (lo, hi) = G.population_bounds(1596, 2, 0.1)
 run = FlipRun(fg, inits, RunConfig(seed=0x5EED0002, pop_lo=lo, pop_hi=hi), bases=bases)
-for it in range(6):
+for it in range(IT):
     s0 = run.stats()
     t = time.time(); run.steps(S); run.sync(); dt = time.time() - t
     s1 = run.stats()
     props = (s1['proposals'] - s0['proposals']).sum()
-    print(f"iter {it}: {dt*1e3:8.1f} ms wall, kernel {run.last_ms():8.1f} ms, proposals {props:.3e} -> {props/dt:.3e}/s, steps/s {C*S/dt:.3e}", flush=True)
-st = run.stats()
-for b in range(10):
-    m = np.arange(C) % 10 == b
-    print(f"base {G.SEC11_BASES[b]:6.3f}: prop/step {st['proposals'][m].sum()/st['steps'][m].sum():5.2f} draws/prop {st['draws'][m].sum()/st['proposals'][m].sum():5.2f} acc/step {st['accepted'][m].sum()/st['steps'][m].sum():5.3f} cut {st['cut'][m].mean():7.1f} bfs {st['bfs_calls'][m].sum()}")
+    if it >= IT - 2:
+        print(f"base_idx {B} iter {it}: kernel {run.last_ms():8.2f} ms, proposals/s {props/dt:.3e}, steps/s {C*S/dt:.3e}, acc/prop {(s1['accepted']-s0['accepted']).sum()/props:.3f}, draws/prop {(s1['draws']-s0['draws']).sum()/props:.2f}", flush=True)
