@@ -20,14 +20,14 @@ FC_ERR_UNSUPPORTED = -4
 FC_ERR_NOMEM = -5
 
 FC_GRAPH_NO_EXACT = 0x1
-FC_PROPOSE_BI_SIGN = 0
+FC_PROPOSE_BI_SIGN, FC_PROPOSE_PAIR = 0, 1
 FC_DIAG_WAIT, FC_DIAG_HIST, FC_DIAG_EDGES, FC_DIAG_FLIPS = 0x1, 0x2, 0x4, 0x8
 FC_FLAG_FORCE_BFS = 0x1
 
 EXPORTED = [
     "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
     "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
-    "fc_run_read_stats", "fc_run_read_state", "fc_run_read_trace", "fc_run_trace_reset", "fc_run_read_hist",
+    "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_trace_reset", "fc_run_read_hist",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_n_chains", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
 ]
@@ -44,7 +44,8 @@ class Params(ctypes.Structure):
                 ("pop_lo", ctypes.c_int64), ("pop_hi", ctypes.c_int64), ("seed", ctypes.c_uint64),
                 ("chain_id_offset", ctypes.c_uint32), ("diag_mask", ctypes.c_uint32),
                 ("flags", ctypes.c_uint32), ("device", ctypes.c_int32), ("trace_chains", ctypes.c_int32),
-                ("trace_cap", ctypes.c_int64), ("labels", _P(ctypes.c_int32)), ("log1mp", _P(ctypes.c_double))]
+                ("trace_cap", ctypes.c_int64), ("labels", _P(ctypes.c_int32)), ("log1mp", _P(ctypes.c_double)),
+                ("wmax", ctypes.c_int32)]
 
 
 class ChainStats(ctypes.Structure):
@@ -102,6 +103,7 @@ def load(build_if_missing: bool = True):
     L.fc_run_timings.argtypes = [vp, _P(ctypes.c_float), i32, _P(i32)]
     L.fc_run_read_stats.argtypes = [vp, _P(ChainStats)]
     L.fc_run_read_state.argtypes = [vp, _P(ctypes.c_int8)]
+    L.fc_run_read_pops.argtypes = [vp, _P(i64)]
     L.fc_run_read_trace.argtypes = [vp, i32, _P(Record), i64, _P(i64)]
     L.fc_run_trace_reset.argtypes = [vp]
     L.fc_run_read_hist.argtypes = [vp, _P(i64), _P(i64)]

@@ -44,6 +44,8 @@ struct fc_run {
     int64_t *d_cut_hist = nullptr, *d_nb_hist = nullptr;
     int64_t *d_edge_acc = nullptr, *d_edge_since = nullptr;
     int64_t *d_num_flips = nullptr, *d_part_sum = nullptr, *d_last_flipped = nullptr;
+    int32_t *d_popk = nullptr;
+    int32_t wmax = 1;
     fc_record *d_trace = nullptr;
     uint32_t *d_tape = nullptr;
     int64_t tape_draws = 0;
@@ -77,7 +79,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc, r->d_edge_since,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -199,8 +201,12 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     if (!out) return fail(FC_ERR_ARG, "fc_run_create: null output");
     *out = nullptr;
     if (!gr || !p || !init_assign || n_chains <= 0) return fail(FC_ERR_ARG, "fc_run_create: null argument or n_chains <= 0");
-    if (p->k != 2) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: round-1 kernels implement k == 2 (BI_SIGN)");
-    if (p->proposal != FC_PROPOSE_BI_SIGN) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: unsupported proposal");
+    if (p->k < 2 || p->k > fc::kMaxKGeneral)
+        return fail(FC_ERR_UNSUPPORTED, "fc_run_create: k must be in [2, 32]");
+    if (p->proposal == FC_PROPOSE_BI_SIGN && p->k != 2)
+        return fail(FC_ERR_ARG, "fc_run_create: slow_reversible_propose_bi flips between two districts (k == 2)");
+    if (p->proposal != FC_PROPOSE_BI_SIGN && p->proposal != FC_PROPOSE_PAIR)
+        return fail(FC_ERR_UNSUPPORTED, "fc_run_create: unsupported proposal");
     const fc::HostGraph &g = gr->h;
     const int32_t n = g.n, E = g.n_edges, R = g.ring_max, k = p->k;
     if (p->pop_lo > INT32_MAX || p->pop_hi > INT32_MAX || p->pop_lo < INT32_MIN || p->pop_hi < INT32_MIN)
@@ -226,7 +232,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     r->n_chains = n_chains;
     r->npad = (n + 15) & ~15;
     r->words = (n + 63) / 64;
-    r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + 3 * r->words * 8 + 4 * 64 * 4;
+    r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + 3 * r->words * 8 + 5 * 64 * 4 + fc::kMaxKGeneral * 4;
+    r->wmax = 1;
+    if (k > 2) r->wmax = p->wmax > 0 ? p->wmax : std::max(1, std::min(g.max_degree, k - 1));
     r->chain_lds_bytes = (r->chain_lds_bytes + 15) & ~15;
     if ((size_t)r->chain_lds_bytes * fc::kWavesPerBlock > 160 * 1024)
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: graph too large for the wave-per-chain LDS layout");
@@ -235,6 +243,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     std::vector<int8_t> assign((size_t)n_chains * r->npad, 0);
     std::vector<uint8_t> fcnt((size_t)n_chains * r->npad, 0);
     std::vector<fc::ChainScalars> sc(n_chains);
+    std::vector<int32_t> popk((size_t)n_chains * fc::kMaxKGeneral, 0);
     std::vector<uint64_t> thresh((size_t)n_chains * (2 * R + 1));
     std::vector<int32_t> q;
     std::vector<uint8_t> seen(n);
@@ -246,9 +255,11 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     for (int32_t c = 0; c < n_chains; ++c) {
         const int8_t *a = init_assign + (size_t)c * n;
         std::memcpy(&assign[(size_t)c * r->npad], a, n);
-        int64_t pops[fc::kMaxK] = {0, 0};
-        int32_t ng[fc::kMaxK] = {0, 0};
+        int64_t pops[fc::kMaxKGeneral] = {0};
+        int32_t ng[fc::kMaxKGeneral] = {0};
         for (int32_t u = 0; u < n; ++u) {
+            if (a[u] < 0 || a[u] >= k)
+                return fail(FC_ERR_ARG, "chain " + std::to_string(c) + ": district id out of range [0, k)");
             pops[a[u]] += g.pop[u];
             if (g.meta[u] & fc::kMetaGamma) ng[a[u]] += 1;
         }
@@ -273,6 +284,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         s.nb = nb;
         s.pops[0] = (int32_t)pops[0];
         s.pops[1] = (int32_t)pops[1];
+        for (int d = 0; d < fc::kMaxKGeneral; ++d) popk[(size_t)c * fc::kMaxKGeneral + d] = (int32_t)pops[d];
         s.ngamma[0] = ng[0];
         s.ngamma[1] = ng[1];
         s.last_flip = -1;
@@ -326,6 +338,8 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     HIP_TRY(hipMemcpy(r->d_assign, assign.data(), assign.size(), hipMemcpyHostToDevice));
     if ((rc = dalloc(&r->d_fcnt, fcnt.size()))) return rc;
     HIP_TRY(hipMemcpy(r->d_fcnt, fcnt.data(), fcnt.size(), hipMemcpyHostToDevice));
+    if ((rc = dalloc(&r->d_popk, popk.size()))) return rc;
+    HIP_TRY(hipMemcpy(r->d_popk, popk.data(), popk.size() * 4, hipMemcpyHostToDevice));
     if ((rc = dalloc(&r->d_sc, sc.size()))) return rc;
     HIP_TRY(hipMemcpy(r->d_sc, sc.data(), sc.size() * sizeof(sc[0]), hipMemcpyHostToDevice));
     if ((rc = dalloc(&r->d_thresh, thresh.size()))) return rc;
@@ -392,6 +406,9 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.n_edges = r->g.n_edges;
     k.n_chains = r->n_chains;
     k.k = r->p.k;
+    k.popk = r->d_popk;
+    k.wmax = r->wmax;
+    k.wthresh = (uint32_t)((1ull << 32) % (uint64_t)r->wmax);
     k.chain_lds_bytes = r->chain_lds_bytes;
     k.words = r->words;
     k.lemire_thresh = (uint32_t)((1ull << 32) % (uint64_t)r->g.n);
@@ -518,6 +535,26 @@ int fc_run_read_state(fc_run *r, int8_t *assign_out) {
     HIP_TRY(hipMemcpy(a.data(), r->d_assign, a.size(), hipMemcpyDeviceToHost));
     for (int32_t c = 0; c < r->n_chains; ++c)
         std::memcpy(assign_out + (size_t)c * r->g.n, &a[(size_t)c * r->npad], r->g.n);
+    return FC_OK;
+}
+
+int fc_run_read_pops(fc_run *r, int64_t *pops_out) {
+    if (!r || !pops_out) return fail(FC_ERR_ARG, "fc_run_read_pops: null argument");
+    if (int rc = fc_run_sync(r)) return rc;
+    const int k = r->p.k;
+    if (k == 2) {
+        std::vector<fc::ChainScalars> sc(r->n_chains);
+        HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+        for (int32_t c = 0; c < r->n_chains; ++c) {
+            pops_out[2 * c] = sc[c].pops[0];
+            pops_out[2 * c + 1] = sc[c].pops[1];
+        }
+    } else {
+        std::vector<int32_t> pk((size_t)r->n_chains * fc::kMaxKGeneral);
+        HIP_TRY(hipMemcpy(pk.data(), r->d_popk, pk.size() * 4, hipMemcpyDeviceToHost));
+        for (int32_t c = 0; c < r->n_chains; ++c)
+            for (int d = 0; d < k; ++d) pops_out[(size_t)c * k + d] = pk[(size_t)c * fc::kMaxKGeneral + d];
+    }
     return FC_OK;
 }
 

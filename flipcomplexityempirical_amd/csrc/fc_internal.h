@@ -12,7 +12,8 @@ namespace fc {
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;   // one chain per wave, 4 chains per 256-thread workgroup
-constexpr int kMaxK = 2;            // round-1 kernels: k = 2 (BI_SIGN)
+constexpr int kMaxK = 2;            // districts held in ChainScalars (k = 2 fast path)
+constexpr int kMaxKGeneral = 32;    // districts of the general (PAIR) kernel
 
 // meta word layout (also exported by fc_graph_rings)
 constexpr uint64_t kMetaLenMask = 0xffull;
@@ -99,7 +100,10 @@ struct KParams {
     int64_t trace_cap;
     const uint32_t *tape;       // replay tape or null
     int64_t tape_draws;
-    int32_t nsub;               // max draw rounds of 64 per batch (1, 2, 4, 8)
+    int32_t *popk;              // [n_chains * 32] district populations (k > 2)
+    int32_t wmax;               // PAIR: foreign-district slots per node draw
+    uint32_t wthresh;           // 2^32 mod wmax
+    int32_t nsub;               // max draw rounds of 64 per batch (1, 2, 4)
     int32_t hit_stop;           // start another round only while fewer boundary hits than this
 };
 

@@ -133,8 +133,10 @@ constexpr uint32_t ST_BR = 32u;  // ... and its result
 
 }  // namespace
 
-template <int RMAX, int NSUB>
-__global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
+// KM = 2: two districts (BI_SIGN, and PAIR with k = 2, which coincide); the outer-face
+// exact rule applies.  KM = 0: k <= 32 districts, PAIR proposals, populations in LDS.
+template <int RMAX, int NSUB, int KM>
+__global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -150,7 +152,8 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
     uint64_t *vis = T + (2 * RMAX + 2);
     uint64_t *front = vis + p.words;
     uint64_t *nxt = front + p.words;
-    uint32_t *slot = (uint32_t *)(nxt + p.words);  // [4][64]: node, word1, word2, draw offset
+    uint32_t *slot = (uint32_t *)(nxt + p.words);  // [5][64]: node, word1, word2, draw offset, word3
+    int32_t *popk = (int32_t *)(slot + 5 * 64);    // [32] district populations (KM = 0)
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
     // ---- load the chain into LDS -------------------------------------------------------
@@ -162,6 +165,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
             ((uint4 *)fcnt)[i] = gf[i];
         }
         if (lane < 2 * RMAX + 1) T[lane] = p.thresh[(size_t)c * (2 * RMAX + 1) + lane];
+        if (KM == 0 && lane < 32) popk[lane] = p.popk[(size_t)c * 32 + lane];
     }
     ChainScalars *scp = p.sc + c;
     uint64_t draw = scp->draw;
@@ -224,6 +228,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
                 slot[64 + pos] = w.x1;
                 slot[128 + pos] = w.x2;
                 slot[192 + pos] = (uint32_t)off;
+                slot[256 + pos] = w.x3;
             }
             rv[r] = v;
             uint64_t nm = __ballot(ok && !hit);
@@ -254,14 +259,43 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
         const uint32_t full = (1u << Ln) - 1u;
         const uint32_t nbr = (uint32_t)(rec.meta >> kMetaNbrShift) & 0xffffu;
         const uint32_t link = (uint32_t)(rec.meta >> kMetaLinkShift) & 0xffffu;
-        uint32_t inA = 0;
+        uint32_t inA = 0;    // ring cells in the old district
+        uint32_t tmask;      // neighbours in the target district
+        int tgt;             // target district
+        bool slot_ok = true;
+        if constexpr (KM == 2) {
 #pragma unroll
-        for (int i = 0; i < RMAX; ++i) inA |= (uint32_t)(a[ring_entry<RMAX>(rec.ring, i)] == av) << i;
-        inA &= full;
+            for (int i = 0; i < RMAX; ++i) inA |= (uint32_t)(a[ring_entry<RMAX>(rec.ring, i)] == av) << i;
+            inA &= full;
+            tgt = 1 - av;                       // -1 * assignment, grid_chain_sec11.py:145
+            tmask = nbr & ~inA;
+        } else {
+            int adv[RMAX];
+            uint32_t dm = 0;                    // foreign districts among the neighbours
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) {
+                adv[i] = a[ring_entry<RMAX>(rec.ring, i)];
+                inA |= (uint32_t)(adv[i] == av) << i;
+                if (((nbr >> i) & 1u) && adv[i] != av) dm |= 1u << adv[i];
+            }
+            inA &= full;
+            // slow_reversible_propose (:117-130): uniform over (node, district) pairs -- slot
+            // r < wmax by an exact Lemire map of word 3; the r-th foreign district is the target
+            const uint64_t mw = (uint64_t)slot[256 + lane] * (uint64_t)(uint32_t)p.wmax;
+            const int r = (int)(mw >> 32);
+            slot_ok = (uint32_t)mw >= p.wthresh && r < __popc(dm);
+            uint32_t dd = dm;
+            for (int q = 0; q < r && dd; ++q) dd &= dd - 1u;
+            tgt = dd ? __builtin_ctz(dd) : 0;
+            tmask = 0;
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) tmask |= (uint32_t)(adv[i] == tgt) << i;
+            tmask &= nbr;
+        }
         const uint32_t nbrA = inA & nbr;
         const int nA = __popc(nbrA);
-        const int nBn = rec.deg - nA;
-        const bool isprop = has && nBn > 0;
+        const int nT = __popc(tmask);
+        const bool isprop = has && (rec.deg - nA) > 0 && slot_ok;
         bool s_lin, s_cyc;
         {
             const uint32_t rot = Ln ? (((inA >> 1) | (inA << (Ln - 1))) & full) : 0u;
@@ -270,14 +304,14 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
             const uint32_t vlink = (Ln >= 2 && (inA & 1u) && ((inA >> (Ln - 1)) & 1u)) ? (1u << (Ln - 1)) : 0u;
             s_cyc = one_run(nbrA, full & ~(lk | vlink), full);
         }
-        const bool exact = (rec.meta & kMetaExact) && !force_bfs;
+        const bool exact = KM == 2 && (rec.meta & kMetaExact) && !force_bfs;
         const bool gam = (rec.meta & kMetaGamma) != 0;
-        const int delta = nA - nBn;
+        const int delta = nA - nT;  // cut(S') - cut(S)
         const bool acc = mant53(w1, w2) < T[delta + RMAX];
-        // packed for the wave-uniform apply: node | A | outer | delta+16 | nA
-        const uint32_t pk = (uint32_t)v | ((uint32_t)av << 15) | ((uint32_t)gam << 16) |
-                            ((uint32_t)(delta + 16) << 17) | ((uint32_t)nA << 22);
+        // packed for the wave-uniform apply
+        const uint32_t pk = (uint32_t)v | ((uint32_t)av << 15) | ((uint32_t)tgt << 21) | ((uint32_t)gam << 27);
         const uint32_t pk2 = inA | (nbr << 16);
+        const uint32_t pk3 = tmask | ((uint32_t)(delta + 32) << 16);  // |delta| <= deg <= 16
 
         // ---- 2. commit loop (wave-uniform) -----------------------------------------------
         uint32_t st = 0;
@@ -302,7 +336,14 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
                 known = s_lin;
                 ok = s_lin;
             }
-            const int pa = av ? pops1 : pops0, pb = av ? pops0 : pops1;
+            int pa, pb;
+            if constexpr (KM == 2) {
+                pa = av ? pops1 : pops0;
+                pb = av ? pops0 : pops1;
+            } else {
+                pa = popk[av];
+                pb = popk[tgt];
+            }
             const bool popok = (pa - pv >= p.pop_lo) && (pb + pv <= p.pop_hi);
             const bool prop = isprop && lane >= pos && lane < end;
             const bool valid = prop && known && ok && popok;
@@ -337,18 +378,18 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
                 }
                 if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
                 const bool res = wave_bfs<RMAX>(G, a, vis, front, nxt, p.words, lane, (int)(pkf & 0x7fffu),
-                                                (int)((pkf >> 15) & 1u), my_target, start, bfs_levels);
+                                                (int)((pkf >> 15) & 63u), my_target, start, bfs_levels);
                 ++bfs_calls;
                 if (lane == f) st |= ST_BD | (res ? ST_BR : 0u);
                 continue;
             }
             // ---- accept slot f: apply the flip -----------------------------------------
-            const uint32_t pkf = rlu(pk, f), pk2f = rlu(pk2, f);
-            const int vf = (int)(pkf & 0x7fffu), Af = (int)((pkf >> 15) & 1u);
-            const bool gamf = (pkf >> 16) & 1u;
-            const int df = (int)((pkf >> 17) & 31u) - 16, nAf = (int)((pkf >> 22) & 31u);
+            const uint32_t pkf = rlu(pk, f), pk2f = rlu(pk2, f), pk3f = rlu(pk3, f);
+            const int vf = (int)(pkf & 0x7fffu), Af = (int)((pkf >> 15) & 63u), tf = (int)((pkf >> 21) & 63u);
+            const bool gamf = (pkf >> 27) & 1u;
+            const int df = (int)(pk3f >> 16) - 32;
             const int pvf = rl32(pv, f);
-            const uint32_t inAf = pk2f & 0xffffu, nbrf = pk2f >> 16;
+            const uint32_t inAf = pk2f & 0xffffu, nbrf = pk2f >> 16, tmf = pk3f & 0xffffu;
             uint32_t rw[RMAX / 2];
 #pragma unroll
             for (int k2 = 0; k2 < RMAX / 2; ++k2) rw[k2] = rlu(rec.ring[k2], f);
@@ -357,22 +398,29 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
             for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((lane >> 1) == k2) ? rw[k2] : sel;
             const int my_e = (int)((sel >> (16 * (lane & 1))) & 0xffffu);
             const bool is_nbr = lane < RMAX && ((nbrf >> lane) & 1u);
-            const bool inA_l = (inAf >> lane) & 1u;
+            // foreign-neighbour counts: u sees v leave A (+1 if u in A) and join t (-1 if u in t)
+            const int dlt = (int)((inAf >> lane) & 1u) - (int)((tmf >> lane) & 1u);
             bool enter = false, leave = false;
-            if (is_nbr) {
+            if (is_nbr && dlt != 0) {
                 const int old = fcnt[my_e];
-                fcnt[my_e] = (uint8_t)(old + (inA_l ? 1 : -1));
-                enter = inA_l && old == 0;
-                leave = !inA_l && old == 1;
+                fcnt[my_e] = (uint8_t)(old + dlt);
+                enter = dlt > 0 && old == 0;
+                leave = dlt < 0 && old == 1;
             }
             uint64_t ent = __ballot(enter);
             const int dnb = __popcll(ent) - __popcll(__ballot(leave));
             if (lane == 0) {
-                a[vf] = (int8_t)(1 - Af);
-                fcnt[vf] = (uint8_t)nAf;
+                a[vf] = (int8_t)tf;
+                fcnt[vf] = (uint8_t)(__popc(nbrf) - __popc(tmf));
+                if constexpr (KM == 0) {
+                    popk[Af] -= pvf;
+                    popk[tf] += pvf;
+                }
             }
-            if (Af == 0) { pops0 -= pvf; pops1 += pvf; } else { pops1 -= pvf; pops0 += pvf; }
-            if (gamf) { if (Af == 0) { --ng0; ++ng1; } else { --ng1; ++ng0; } }
+            if constexpr (KM == 2) {
+                if (Af == 0) { pops0 -= pvf; pops1 += pvf; } else { pops1 -= pvf; pops0 += pvf; }
+                if (gamf) { if (Af == 0) { --ng0; ++ng1; } else { --ng1; ++ng0; } }
+            }
             cut += df;
             nb += dnb;
             --rem;
@@ -496,7 +544,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
                 if (is_acc) {
                     const int64_t t_last = t_acc + run_len - 1;
                     const int64_t old = (int64_t)atomicExch(lf + v, (unsigned long long)t_last);
-                    atomicAdd((unsigned long long *)(ps + v), (unsigned long long)(-(int64_t)p.labels[1 - av] * (t_last - old)));
+                    atomicAdd((unsigned long long *)(ps + v), (unsigned long long)(-(int64_t)p.labels[tgt] * (t_last - old)));
                     atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
                 }
             }
@@ -508,7 +556,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
                     const int e = p.ring_eid[(size_t)v * RMAX + i];
                     if ((inA >> i) & 1u) {
                         atomicExch(es + e, (unsigned long long)t_acc);             // becomes cut
-                    } else {
+                    } else if ((tmask >> i) & 1u) {
                         const int64_t since = (int64_t)atomicAdd(es + e, 0ull);    // becomes uncut
                         atomicAdd((unsigned long long *)(ea + e), (unsigned long long)(t_acc - since));
                     }
@@ -527,7 +575,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
                 const bool valid = (st & ST_VS) != 0;
                 rr.draw = (int64_t)d;
                 rr.v = v;
-                rr.flags = valid ? (1 | (is_acc ? 2 : 0)) : ((st & ST_IC) ? 4 : 8);
+                rr.flags = (valid ? (1 | (is_acc ? 2 : 0)) : ((st & ST_IC) ? 4 : 8)) | (tgt << 8);
                 rr.cut = mine ? c_j : cut0;
                 rr.nb = mine ? n_j : nb0;
                 rr.wait = valid ? (mine ? (int64_t)w_j : wait_cur) : 0;
@@ -547,6 +595,7 @@ __global__ __launch_bounds__(256) void flip_k2_kernel(KParams p) {
             ga[i] = ((const uint4 *)a)[i];
             gf[i] = ((const uint4 *)fcnt)[i];
         }
+        if (KM == 0 && lane < 32) p.popk[(size_t)c * 32 + lane] = popk[lane];
     }
     int64_t cnt_prop = n_prop, cnt_acc = n_acc, cnt_ic = n_ic, cnt_ip = n_ip;
 #pragma unroll
@@ -593,24 +642,22 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream) {
     const size_t lds = (size_t)p.chain_lds_bytes * kWavesPerBlock;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(blocks), block(kWave * kWavesPerBlock);
-#define FC_LAUNCH(R, S) hipLaunchKernelGGL((flip_k2_kernel<R, S>), grid, block, lds, s, p)
+#define FC_LAUNCH(R, S, K) hipLaunchKernelGGL((flip_kernel<R, S, K>), grid, block, lds, s, p)
+#define FC_NSUB_SWITCH(R, K)                          \
+    switch (p.nsub) {                                 \
+        case 1: FC_LAUNCH(R, 1, K); break;            \
+        case 2: FC_LAUNCH(R, 2, K); break;            \
+        case 4: FC_LAUNCH(R, 4, K); break;            \
+        default: return (int)hipErrorInvalidValue;    \
+    }
     if (ring_max == 8) {
-        switch (p.nsub) {
-            case 1: FC_LAUNCH(8, 1); break;
-            case 2: FC_LAUNCH(8, 2); break;
-            case 4: FC_LAUNCH(8, 4); break;
-            default: return (int)hipErrorInvalidValue;
-        }
+        if (p.k == 2) { FC_NSUB_SWITCH(8, 2) } else { FC_NSUB_SWITCH(8, 0) }
     } else if (ring_max == 16) {
-        switch (p.nsub) {
-            case 1: FC_LAUNCH(16, 1); break;
-            case 2: FC_LAUNCH(16, 2); break;
-            case 4: FC_LAUNCH(16, 4); break;
-            default: return (int)hipErrorInvalidValue;
-        }
+        if (p.k == 2) { FC_NSUB_SWITCH(16, 2) } else { FC_NSUB_SWITCH(16, 0) }
     } else {
         return (int)hipErrorInvalidValue;
     }
+#undef FC_NSUB_SWITCH
 #undef FC_LAUNCH
     return (int)hipGetLastError();
 }

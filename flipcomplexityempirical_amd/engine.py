@@ -97,6 +97,8 @@ class RunConfig:
     trace_chains: int = 0
     trace_cap: int = 0
     labels: Sequence[int] = (-1, 1)
+    proposal: int = _lib.FC_PROPOSE_BI_SIGN
+    wmax: int = 0
 
 
 class FlipRun:
@@ -122,7 +124,7 @@ class FlipRun:
         self._bases = None if bases is None else np.ascontiguousarray(bases, dtype=np.float64)
         if self._bases is not None and self._bases.shape[0] != self.n_chains:
             raise ValueError("bases must have one entry per chain")
-        prm = _lib.Params(k=cfg.k, proposal=_lib.FC_PROPOSE_BI_SIGN, base=float(cfg.base),
+        prm = _lib.Params(k=cfg.k, proposal=int(cfg.proposal), base=float(cfg.base), wmax=int(cfg.wmax),
                           pop_lo=int(cfg.pop_lo), pop_hi=int(cfg.pop_hi), seed=int(cfg.seed),
                           chain_id_offset=int(cfg.chain_id_offset), diag_mask=int(cfg.diag_mask),
                           flags=int(cfg.flags), device=int(cfg.device), trace_chains=int(cfg.trace_chains),
@@ -176,6 +178,11 @@ class FlipRun:
     def state(self) -> np.ndarray:
         out = np.zeros((self.n_chains, self.graph.n), dtype=np.int8)
         check(_lib.load().fc_run_read_state(self.handle, _p(out, ctypes.c_int8)), "fc_run_read_state")
+        return out
+
+    def pops(self) -> np.ndarray:
+        out = np.zeros((self.n_chains, self.cfg.k), dtype=np.int64)
+        check(_lib.load().fc_run_read_pops(self.handle, _p(out, ctypes.c_int64)), "fc_run_read_pops")
         return out
 
     def trace(self, chain: int = 0) -> np.ndarray:

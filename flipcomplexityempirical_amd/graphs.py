@@ -208,6 +208,24 @@ def triangular_graph(m: int, n: int) -> GraphSpec:
     return from_networkx(H)
 
 
+def quadrant_plan(nodes: Sequence, half: float = 20) -> Dict:
+    """C3's k=4 start plan on the sec11 lattice: district ``(x >= half) + 2 (y >= half)``
+    (labels 0..3)."""
+    return {n: int(n[0] >= half) + 2 * int(n[1] >= half) for n in nodes}
+
+
+def strip_plan(spec: GraphSpec, k: int) -> Dict:
+    """k vertical strips of (nearly) equal node count by x-coordinate, ties by y
+    (C4's k=8 start plan on the triangular lattice; labels 0..k-1)."""
+    if spec.pos is None:
+        raise ValueError("strip_plan needs node positions")
+    order = np.lexsort((spec.pos[:, 1], spec.pos[:, 0]))
+    out = {}
+    for rank, i in enumerate(order):
+        out[spec.nodes[int(i)]] = int(rank * k // spec.n)
+    return out
+
+
 # --------------------------------------------------------------------------------------
 # Known answers used by tests (host-side, networkx)
 # --------------------------------------------------------------------------------------

@@ -42,6 +42,7 @@ extern "C" {
 
 /* fc_params.proposal */
 #define FC_PROPOSE_BI_SIGN 0     /* slow_reversible_propose_bi, grid_chain_sec11.py:132-145 */
+#define FC_PROPOSE_PAIR 1        /* slow_reversible_propose,    grid_chain_sec11.py:117-130 */
 
 /* fc_params.diag_mask: per-yield driver diagnostics kept on the device
  * (grid_chain_sec11.py:350-419).  The streaming sums are always kept.                    */
@@ -68,7 +69,7 @@ typedef struct fc_graph_info {
 } fc_graph_info;
 
 typedef struct fc_params {
-    int32_t k;                 /* districts; round 1 kernels: k == 2                        */
+    int32_t k;                 /* districts: 2 (BI_SIGN or PAIR) or 3..32 (PAIR)            */
     int32_t proposal;          /* FC_PROPOSE_*                                              */
     double base;               /* cut_accept base when `bases` is NULL (:171-179, :279-280) */
     int64_t pop_lo, pop_hi;    /* inclusive integer bounds equivalent to
@@ -82,6 +83,7 @@ typedef struct fc_params {
     int64_t trace_cap;         /* records per traced chain                                  */
     const int32_t *labels;     /* [k] reference district labels (e.g. -1, 1); NULL = 0..k-1 */
     const double *log1mp;      /* [n+1] log(1 - b/(N^k - 1)); NULL = computed in double     */
+    int32_t wmax;              /* PAIR: district slots per node draw (<= 0: min(max deg, k-1)) */
 } fc_params;
 
 /* Per-chain statistics.  "Yields" are the states a `for part in exp_chain` loop sees:
@@ -152,6 +154,8 @@ int fc_run_last_ms(fc_run *r, float *ms);
 int fc_run_timings(fc_run *r, float *ms, int32_t cap, int32_t *n);
 int fc_run_read_stats(fc_run *r, fc_chain_stats *out);
 int fc_run_read_state(fc_run *r, int8_t *assign_out);
+/* District populations [c * k] (Tally('population'), :299). */
+int fc_run_read_pops(fc_run *r, int64_t *pops_out);
 int fc_run_read_trace(fc_run *r, int32_t chain, fc_record *out, int64_t cap, int64_t *len);
 /* Restart every traced chain's record buffer at 0 (chunked per-step iteration). */
 int fc_run_trace_reset(fc_run *r);

@@ -184,8 +184,10 @@ static void yield_state(ctx_t *c, fr_stats *st, fr_outputs *o, int64_t t) {
 }
 
 int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outputs *o) {
-    if (!p || !init_assign || !st || p->n <= 0 || p->k != 2 || !p->row_ptr || !p->col_idx || !p->pop)
+    if (!p || !init_assign || !st || p->n <= 0 || p->k < 2 || p->k > 64 || !p->row_ptr || !p->col_idx || !p->pop)
         return -2;
+    if (p->proposal == FR_PROPOSE_BI_SIGN && p->k != 2) return -2;
+    if (p->proposal != FR_PROPOSE_BI_SIGN && p->proposal != FR_PROPOSE_PAIR) return -2;
     if (o && o->num_flips && (!o->part_sum || !o->last_flipped || !p->labels)) return -2;
     const int32_t n = p->n;
     memset(st, 0, sizeof *st);
@@ -237,6 +239,16 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
     yield_state(&c, st, o, 0);                                   /* yield #0 = S0 */
 
     const uint32_t thresh = (uint32_t)((0x100000000ull) % (uint64_t)n);
+    /* PAIR: a global slot count wmax >= every node's number of foreign districts */
+    int32_t wmax = 1;
+    if (p->proposal == FR_PROPOSE_PAIR) {
+        int32_t maxdeg = 0;
+        for (int32_t u = 0; u < n; ++u)
+            if (p->row_ptr[u + 1] - p->row_ptr[u] > maxdeg) maxdeg = p->row_ptr[u + 1] - p->row_ptr[u];
+        wmax = p->wmax > 0 ? p->wmax : (maxdeg < p->k - 1 ? maxdeg : p->k - 1);
+        if (wmax < 1) wmax = 1;
+    }
+    const uint32_t wthresh = (uint32_t)((0x100000000ull) % (uint64_t)wmax);
     int64_t d = 0;
     while (st->steps < p->n_steps) {
         if ((p->max_draws > 0 && st->draws >= p->max_draws) || (p->tape && d >= p->tape_draws)) {
@@ -250,8 +262,29 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
         if ((uint32_t)m < thresh) continue;                   /* Lemire: exact uniform node */
         const int32_t v = (int32_t)(m >> 32);
         if (!in_boundary(&c, v)) continue;                      /* not in b_nodes_bi        */
+        const int8_t A = c.a[v];
+        int8_t T;
+        if (p->proposal == FR_PROPOSE_BI_SIGN) {
+            T = (int8_t)(1 - A);                                /* -1 * assignment (:145)   */
+        } else {
+            /* slow_reversible_propose (:117-130): uniform over (node, foreign district)
+             * pairs = uniform node, then slot r < wmax accepted iff r < |D(v)|; D(v) in
+             * ascending district order. */
+            const uint64_t mw = (uint64_t)w[3] * (uint64_t)wmax;
+            if ((uint32_t)mw < wthresh) continue;
+            const int32_t r = (int32_t)(mw >> 32);
+            uint64_t dm = 0;
+            for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) {
+                int8_t aw = c.a[p->col_idx[j]];
+                if (aw != A) dm |= 1ull << aw;
+            }
+            int32_t cnt = 0;
+            T = -1;
+            for (int32_t dd = 0; dd < p->k; ++dd)
+                if (dm >> dd & 1ull) { if (cnt == r) { T = (int8_t)dd; break; } ++cnt; }
+            if (T < 0) continue;                                 /* slot beyond |D(v)|      */
+        }
         st->proposals += 1;
-        const int8_t A = c.a[v], T = (int8_t)(1 - A);
         int32_t flags = 0;
         if (!flip_contiguous_ctx(&c, v)) {
             st->inv_contig += 1; flags = 4;
@@ -265,7 +298,7 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
         if (flags) {
             if (o && o->trace && o->trace_len < o->trace_cap) {
                 fr_record *r = &o->trace[o->trace_len++];
-                r->draw = draw; r->v = v; r->flags = flags; r->cut = c.cut; r->nb = c.nb; r->wait = 0;
+                r->draw = draw; r->v = v; r->flags = flags | (T << 8); r->cut = c.cut; r->nb = c.nb; r->wait = 0;
             }
             continue;
         }
@@ -297,7 +330,7 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
         yield_state(&c, st, o, st->steps);
         if (o && o->trace && o->trace_len < o->trace_cap) {
             fr_record *r = &o->trace[o->trace_len++];
-            r->draw = draw; r->v = v; r->flags = 1 | (acc ? 2 : 0); r->cut = c.cut; r->nb = c.nb;
+            r->draw = draw; r->v = v; r->flags = 1 | (acc ? 2 : 0) | (T << 8); r->cut = c.cut; r->nb = c.nb;
             r->wait = st->wait_cur;
         }
     }

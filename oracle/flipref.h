@@ -35,7 +35,8 @@ extern "C" {
 typedef struct fr_record {
     int64_t draw;   /* draw index of this proposal                          */
     int32_t v;      /* proposed node (canonical index)                      */
-    int32_t flags;  /* 1 valid, 2 accepted, 4 invalid: contiguity, 8 invalid: population */
+    int32_t flags;  /* 1 valid, 2 accepted, 4 invalid: contiguity, 8 invalid: population;
+                       bits 8-15: target district                                  */
     int32_t cut;    /* |cut edges| of the state after this proposal           */
     int32_t nb;     /* |boundary nodes| after this proposal                   */
     int64_t wait;   /* geometric wait of the yielded state (valid proposals) */
@@ -77,7 +78,12 @@ typedef struct fr_params {
     int64_t n_steps;           /* valid steps to advance                           */
     int64_t max_draws;         /* stuck cap (<=0: unlimited)                       */
     const double *log1mp;      /* [n+1] log(1-|B|/(N^k-1)); NULL => waits are 0    */
+    int32_t proposal;          /* FR_PROPOSE_BI_SIGN (k == 2) or FR_PROPOSE_PAIR   */
+    int32_t wmax;              /* PAIR slot count (<= 0: min(max degree, k - 1))   */
 } fr_params;
+
+#define FR_PROPOSE_BI_SIGN 0   /* slow_reversible_propose_bi, grid_chain_sec11.py:132-145 */
+#define FR_PROPOSE_PAIR 1      /* slow_reversible_propose,    grid_chain_sec11.py:117-130 */
 
 typedef struct fr_outputs {
     fr_record *trace; int64_t trace_cap; int64_t trace_len;   /* nullable trace      */

@@ -109,7 +109,10 @@ class FrParams(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("chain_id", ctypes.c_uint32),
                 ("tape", _P(ctypes.c_uint32)), ("tape_draws", ctypes.c_int64),
                 ("n_steps", ctypes.c_int64), ("max_draws", ctypes.c_int64),
-                ("log1mp", _P(ctypes.c_double))]
+                ("log1mp", _P(ctypes.c_double)), ("proposal", ctypes.c_int32), ("wmax", ctypes.c_int32)]
+
+
+PROPOSE_BI_SIGN, PROPOSE_PAIR = 0, 1
 
 
 class FrOutputs(ctypes.Structure):
@@ -171,11 +174,13 @@ class CRef:
             seed: int, chain_id: int, n_steps: int, k: int = 2, labels=(-1, 1),
             log1mp: Optional[np.ndarray] = None, tape: Optional[np.ndarray] = None,
             max_draws: int = 0, trace_cap: int = 0, want_hist: bool = False,
-            want_edges: bool = False, want_flips: bool = False) -> Dict:
+            want_edges: bool = False, want_flips: bool = False, proposal: int = 0, wmax: int = 0) -> Dict:
         n, E = spec.n, spec.n_edges
         row_ptr = np.ascontiguousarray(spec.row_ptr, dtype=np.int32)
         col_idx = np.ascontiguousarray(spec.col_idx, dtype=np.int32)
         pop = np.ascontiguousarray(spec.pop, dtype=np.int32)
+        if labels is None or len(labels) != k:
+            labels = list(range(k))
         lab = np.ascontiguousarray(labels, dtype=np.int32)
         init = np.ascontiguousarray(init_assign, dtype=np.int8)
         l1 = None if log1mp is None else np.ascontiguousarray(log1mp, dtype=np.float64)
@@ -185,7 +190,8 @@ class CRef:
                      base=float(base), pop_lo=int(pop_lo), pop_hi=int(pop_hi), seed=int(seed),
                      chain_id=int(chain_id), tape=_ptr(tp, ctypes.c_uint32),
                      tape_draws=0 if tp is None else tp.shape[0] // 6,
-                     n_steps=int(n_steps), max_draws=int(max_draws), log1mp=_ptr(l1, ctypes.c_double))
+                     n_steps=int(n_steps), max_draws=int(max_draws), log1mp=_ptr(l1, ctypes.c_double),
+                     proposal=int(proposal), wmax=int(wmax))
         trace = np.zeros(trace_cap, dtype=RECORD_DTYPE) if trace_cap else None
         final = np.zeros(n, dtype=np.int8)
         cut_hist = np.zeros(E + 1, dtype=np.int64) if want_hist else None
@@ -279,6 +285,12 @@ def _cut_edges(partition):  # gerrychain.updaters.cut_edges [gc-0.2]
     return (parent_cut | new_cuts) - obsolete
 
 
+def _b_nodes_pairs(partition):  # b_nodes, grid_chain_sec11.py:151-153
+    a = partition.assignment
+    cut = partition["cut_edges"]
+    return {(x[0], a[x[1]]) for x in cut}.union({(x[1], a[x[0]]) for x in cut})
+
+
 def _b_nodes_bi(partition):  # grid_chain_sec11.py:155-156
     return {x[0] for x in partition["cut_edges"]}.union({x[1] for x in partition["cut_edges"]})
 
@@ -323,7 +335,8 @@ class GcFaithfulChain:
     stream (Philox or a tape): node-tape replay of ``slow_reversible_propose_bi``."""
 
     def __init__(self, spec, plan: Dict, *, base: float, pop_bounds, seed: int, chain_id: int,
-                 log1mp: Optional[np.ndarray] = None, tape: Optional[np.ndarray] = None):
+                 log1mp: Optional[np.ndarray] = None, tape: Optional[np.ndarray] = None,
+                 pair: bool = False, wmax: int = 0):
         self.spec = spec
         self.g = spec.nx_graph
         self.base = base
@@ -332,11 +345,15 @@ class GcFaithfulChain:
         self.log1mp = log1mp
         self.tape = tape
         self.labels = sorted(set(plan.values()))
-        ups = {"population": _population, "cut_edges": _cut_edges, "b_nodes": _b_nodes_bi}
+        ups = {"population": _population, "cut_edges": _cut_edges, "b_nodes": _b_nodes_bi, "pairs": _b_nodes_pairs}
         self.state = _Partition(self.g, assignment=plan, updaters=ups)
         self.d = 0
         self.n = spec.n
         self.thresh = (1 << 32) % self.n
+        self.pair = pair
+        k = len(self.labels)
+        self.wmax = wmax if wmax > 0 else max(1, min(int(spec.degree().max()), k - 1))
+        self.wthresh = (1 << 32) % self.wmax
         self.stats = dict(steps=0, proposals=0, draws=0, accepted=0, inv_contig=0, inv_pop=0,
                           sum_cut=0, sum_nb=0, sum_wait=0)
         self.trace = []
@@ -387,13 +404,27 @@ class GcFaithfulChain:
             s = self.state
             if node not in s["b_nodes"]:
                 continue
+            if self.pair:
+                # slow_reversible_propose (:117-130): uniform over the (node, district) pairs
+                # of b_nodes (:151-153) -- canonical: slot r < wmax, r-th foreign district
+                mw = w[3] * self.wmax
+                if (mw & 0xFFFFFFFF) < self.wthresh:
+                    continue
+                foreign = sorted({d for (x, d) in s["pairs"] if x == node}, key=self.labels.index)
+                r = mw >> 32
+                if r >= len(foreign):
+                    continue
+                target = foreign[r]
+            else:
+                target = -1 * s.assignment[node]  # :145 (labels are ±1)
+            tid = self.labels.index(target) << 8
             self.stats["proposals"] += 1
-            proposal = s.flip({node: -1 * s.assignment[node]})  # :145 (labels are ±1)
+            proposal = s.flip({node: target})
             s.parent = None  # MarkovChain.__next__ erases the grandparent [gc-0.2]
             bad = self._valid(proposal)
             if bad:
                 self.stats["inv_contig" if bad == FLAG_INV_CONTIG else "inv_pop"] += 1
-                self.trace.append((draw, self.spec.index[node], bad, len(s["cut_edges"]), len(s["b_nodes"]), 0))
+                self.trace.append((draw, self.spec.index[node], bad | tid, len(s["cut_edges"]), len(s["b_nodes"]), 0))
                 continue
             self.stats["steps"] += 1
             bound = self.base ** (-len(proposal["cut_edges"]) + len(s["cut_edges"]))  # :175
@@ -404,7 +435,7 @@ class GcFaithfulChain:
                 self.wait = self._geom(draw, 1)
             self._yield()
             cur = self.state
-            self.trace.append((draw, self.spec.index[node], FLAG_VALID | (FLAG_ACCEPTED if acc else 0),
+            self.trace.append((draw, self.spec.index[node], FLAG_VALID | (FLAG_ACCEPTED if acc else 0) | tid,
                                len(cur["cut_edges"]), len(cur["b_nodes"]), self.wait))
             return cur
 

@@ -64,3 +64,41 @@ def test_oracle_stuck_cap(cref, sec11):
     r = cref.run(sec11, a0, base=1.0, pop_lo=798, pop_hi=798, seed=0, chain_id=0, n_steps=10, max_draws=5000)
     assert r["rc"] == 1 and r["stats"]["stuck"] == 1 and r["stats"]["steps"] == 0
     assert r["stats"]["inv_pop"] > 0
+
+
+@pytest.mark.parametrize("which,k,base", [("sec11", 4, G.SEC11_MU), ("sec11", 4, 0.5), ("tri", 8, 1.0)])
+def test_c_oracle_pair_equals_gc_faithful(cref, sec11, which, k, base):
+    """PAIR proposals (slow_reversible_propose over b_nodes pairs, grid_chain_sec11.py:117-130,
+    151-153) for k > 2: the C restatement equals the gerrychain-faithful one."""
+    from oracle.flipref import GcFaithfulChain
+    spec = sec11 if which == "sec11" else G.triangular_graph(12, 22)
+    plan = G.quadrant_plan(spec.nodes) if which == "sec11" else G.strip_plan(spec, k)
+    labels = list(range(k))
+    a0 = spec.assignment_array(plan, labels)
+    l1 = G.log1mp_table(spec.n, k)
+    pct = 0.05 if which == "sec11" else 0.1
+    (lo, hi), (ilo, ihi) = G.population_bounds(int(spec.pop.sum()), k, pct)
+    gc = GcFaithfulChain(spec, plan, base=base, pop_bounds=(lo, hi), seed=5, chain_id=2, log1mp=l1,
+                         pair=True).run(300)
+    r = cref.run(spec, a0, base=base, pop_lo=ilo, pop_hi=ihi, seed=5, chain_id=2, n_steps=300, k=k,
+                 labels=labels, log1mp=l1, trace_cap=100000, proposal=1)
+    gtr = np.array(gc.trace, dtype=np.int64)
+    tr = r["trace"]
+    assert len(tr) == len(gtr) and len(tr) > 300
+    for i, f in enumerate(["draw", "v", "flags", "cut", "nb", "wait"]):
+        assert np.array_equal(tr[f], gtr[:, i]), f
+    assert np.array_equal(gc.assignment_ids(), r["final"])
+    for key in ("steps", "proposals", "draws", "accepted", "inv_contig", "inv_pop", "sum_cut", "sum_nb", "sum_wait"):
+        assert gc.stats[key] == r["stats"][key], key
+
+
+def test_pair_k2_equals_bi_sign(cref, sec11):
+    """With k = 2 the pair set has one district per boundary node: PAIR == BI_SIGN."""
+    l1 = G.log1mp_table(sec11.n, 2)
+    a0 = sec11.assignment_array(G.sec11_plan(1, sec11.nodes), [-1, 1])
+    _, (lo, hi) = G.population_bounds(sec11.n, 2, 0.1)
+    kw = dict(base=0.8, pop_lo=lo, pop_hi=hi, seed=4, chain_id=7, n_steps=1500, log1mp=l1, trace_cap=100000)
+    r0 = cref.run(sec11, a0, proposal=0, **kw)
+    r1 = cref.run(sec11, a0, proposal=1, **kw)
+    assert np.array_equal(r0["trace"], r1["trace"])
+    assert r0["stats"] == r1["stats"]

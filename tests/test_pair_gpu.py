@@ -1,0 +1,112 @@
+"""GPU parity for PAIR proposals (k >= 2; slow_reversible_propose, grid_chain_sec11.py:117-130,
+b_nodes pairs :151-153): the general-k kernel against the C oracle, bit-exact per proposal.
+
+Covers BASELINE configs C3 (sec11 lattice, k=4 quadrant plan, pop tolerance 0.05, base mu)
+and C4 (triangular lattice, k=8 vertical strips) at test sizes, plus PAIR == BI_SIGN at k=2.
+"""
+import numpy as np
+import pytest
+
+from flipcomplexityempirical_amd import graphs as G
+from flipcomplexityempirical_amd import _lib
+from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+
+pytestmark = pytest.mark.gpu
+
+STAT_KEYS = ["steps", "proposals", "draws", "accepted", "inv_contig", "inv_pop", "sum_cut", "sum_nb",
+             "sum_wait", "cut", "nb"]
+ALL_DIAG = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
+
+
+def _run_pair(spec, inits, bases, k, *, steps, pct, seed=21, flags=0, chunks=1, exact=True, proposal=None):
+    fg = FlipGraph(spec, exact=exact)
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
+    cfg = RunConfig(k=k, labels=tuple(range(k)), proposal=_lib.FC_PROPOSE_PAIR if proposal is None else proposal,
+                    seed=seed, pop_lo=lo, pop_hi=hi, diag_mask=ALL_DIAG, flags=flags,
+                    trace_chains=inits.shape[0], trace_cap=400000)
+    run = FlipRun(fg, inits, cfg, bases=bases)
+    per = steps // chunks
+    for i in range(chunks):
+        run.steps(per if i < chunks - 1 else steps - per * (chunks - 1))
+    return run
+
+
+def _check(cref, spec, run, k, inits, bases, *, steps, pct, seed=21):
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
+    st = run.stats()
+    pops = run.pops()
+    ch, nh = run.hist()
+    ct = run.cut_times()
+    nf, ps, lf = run.flips()
+    state = run.state()
+    for c in range(inits.shape[0]):
+        ref = cref.run(spec, inits[c], base=float(bases[c]), pop_lo=lo, pop_hi=hi, seed=seed, chain_id=c,
+                       n_steps=steps, k=k, labels=list(range(k)), log1mp=G.log1mp_table(spec.n, k),
+                       trace_cap=500000, want_hist=True, want_edges=True, want_flips=True, proposal=1)
+        tr, rt = run.trace(c), ref["trace"]
+        assert len(tr) == len(rt), f"chain {c}: {len(tr)} vs {len(rt)} proposals"
+        for f in ("draw", "v", "flags", "cut", "nb", "wait"):
+            bad = np.nonzero(tr[f] != rt[f])[0]
+            assert bad.size == 0, f"chain {c} field {f} first mismatch at {bad[:1]}: {tr[bad[:3]]} vs {rt[bad[:3]]}"
+        for key in STAT_KEYS:
+            assert int(st[key][c]) == int(ref["stats"][key]), f"chain {c} stat {key}"
+        assert np.array_equal(state[c], ref["final"])
+        _, _, p_ref = G.cut_and_boundary(spec, ref["final"])
+        assert np.array_equal(pops[c], np.resize(p_ref, k))
+        assert np.array_equal(ch[c], ref["cut_hist"]) and np.array_equal(nh[c], ref["nb_hist"])
+        assert np.array_equal(ct[c], ref["cut_times"])
+        assert np.array_equal(nf[c], ref["num_flips"]) and np.array_equal(lf[c], ref["last_flipped"])
+        assert np.array_equal(ps[c], ref["part_sum"])
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_c3_sec11_k4_pair_parity(gpu, cref, sec11, chunks):
+    k, n_chains, steps = 4, 16, 2500
+    a0 = sec11.assignment_array(G.quadrant_plan(sec11.nodes), list(range(k)))
+    inits = np.stack([a0] * n_chains)
+    bases = np.asarray([[G.SEC11_MU, 1.0, 0.5, 4.0][c % 4] for c in range(n_chains)])
+    run = _run_pair(sec11, inits, bases, k, steps=steps, pct=0.05, chunks=chunks)
+    _check(cref, sec11, run, k, inits, bases, steps=steps, pct=0.05)
+
+
+def test_c3_force_bfs(gpu, cref, sec11):
+    k = 4
+    a0 = sec11.assignment_array(G.quadrant_plan(sec11.nodes), list(range(k)))
+    inits = np.stack([a0] * 8)
+    bases = np.asarray([0.3, 1.0, G.SEC11_MU, 8.0] * 2)
+    run = _run_pair(sec11, inits, bases, k, steps=1500, pct=0.05, flags=_lib.FC_FLAG_FORCE_BFS)
+    assert run.stats()["bfs_calls"].sum() > 0
+    _check(cref, sec11, run, k, inits, bases, steps=1500, pct=0.05)
+
+
+@pytest.mark.parametrize("m,n", [(20, 38), (40, 78)])
+def test_c4_triangular_k8_pair_parity(gpu, cref, m, n):
+    spec = G.triangular_graph(m, n)
+    k = 8
+    a0 = spec.assignment_array(G.strip_plan(spec, k), list(range(k)))
+    inits = np.stack([a0] * 8)
+    bases = np.asarray([1 / 2.0, 1.0, 2.0, 4.0] * 2)
+    run = _run_pair(spec, inits, bases, k, steps=2000, pct=0.1)
+    _check(cref, spec, run, k, inits, bases, steps=2000, pct=0.1)
+
+
+def test_pair_k2_equals_bi_sign_gpu(gpu, sec11):
+    k = 2
+    inits = np.stack([sec11.assignment_array(G.sec11_plan(c % 3, sec11.nodes), [-1, 1]) for c in range(12)])
+    bases = np.asarray(G.SEC11_BASES[:6] * 2)
+    r0 = _run_pair(sec11, inits, bases, k, steps=2000, pct=0.1, proposal=_lib.FC_PROPOSE_BI_SIGN)
+    r1 = _run_pair(sec11, inits, bases, k, steps=2000, pct=0.1)
+    for c in range(12):
+        assert np.array_equal(r0.trace(c), r1.trace(c))
+    assert np.array_equal(r0.state(), r1.state())
+
+
+def test_pair_rejects_bad_config(gpu, sec11):
+    fg = FlipGraph(sec11)
+    a0 = sec11.assignment_array(G.quadrant_plan(sec11.nodes), [0, 1, 2, 3])[None, :]
+    with pytest.raises(ValueError):  # BI_SIGN only flips between two districts
+        FlipRun(fg, a0, RunConfig(k=4, labels=(0, 1, 2, 3), proposal=_lib.FC_PROPOSE_BI_SIGN,
+                                  pop_lo=0, pop_hi=10 ** 6))
+    with pytest.raises(NotImplementedError):
+        FlipRun(fg, a0, RunConfig(k=40, labels=tuple(range(40)), proposal=_lib.FC_PROPOSE_PAIR,
+                                  pop_lo=0, pop_hi=10 ** 6))
