@@ -21,14 +21,15 @@ FC_ERR_NOMEM = -5
 
 FC_GRAPH_NO_EXACT = 0x1
 FC_PROPOSE_BI_SIGN, FC_PROPOSE_PAIR = 0, 1
-FC_DIAG_WAIT, FC_DIAG_HIST, FC_DIAG_EDGES, FC_DIAG_FLIPS = 0x1, 0x2, 0x4, 0x8
+FC_DIAG_WAIT, FC_DIAG_HIST, FC_DIAG_EDGES, FC_DIAG_FLIPS, FC_DIAG_SERIES = 0x1, 0x2, 0x4, 0x8, 0x10
 FC_FLAG_FORCE_BFS = 0x1
 
 EXPORTED = [
     "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
     "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
     "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_trace_reset", "fc_run_read_hist",
-    "fc_run_read_edges", "fc_run_read_flips", "fc_run_n_chains", "fc_run_destroy",
+    "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
+    "fc_run_n_chains", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
 ]
 
@@ -45,7 +46,8 @@ class Params(ctypes.Structure):
                 ("chain_id_offset", ctypes.c_uint32), ("diag_mask", ctypes.c_uint32),
                 ("flags", ctypes.c_uint32), ("device", ctypes.c_int32), ("trace_chains", ctypes.c_int32),
                 ("trace_cap", ctypes.c_int64), ("labels", _P(ctypes.c_int32)), ("log1mp", _P(ctypes.c_double)),
-                ("wmax", ctypes.c_int32)]
+                ("wmax", ctypes.c_int32), ("hit_lo", ctypes.c_int32), ("hit_hi", ctypes.c_int32),
+                ("event_cap", ctypes.c_int64)]
 
 
 class ChainStats(ctypes.Structure):
@@ -55,7 +57,13 @@ class ChainStats(ctypes.Structure):
                 ("sum_cut2", ctypes.c_int64), ("sum_nb2", ctypes.c_int64), ("wait_cur", ctypes.c_int64),
                 ("bfs_calls", ctypes.c_int64), ("bfs_levels", ctypes.c_int64),
                 ("cut", ctypes.c_int32), ("nb", ctypes.c_int32), ("last_flip", ctypes.c_int32),
-                ("stuck", ctypes.c_int32)]
+                ("stuck", ctypes.c_int32), ("hit_time", ctypes.c_int64), ("events", ctypes.c_int64),
+                ("series_t0", ctypes.c_int64), ("series_cut0", ctypes.c_int32), ("series_nb0", ctypes.c_int32)]
+
+
+class Event(ctypes.Structure):
+    _fields_ = [("t", ctypes.c_int64), ("v", ctypes.c_uint16), ("cut", ctypes.c_uint16), ("nb", ctypes.c_uint16),
+                ("target", ctypes.c_uint8), ("reserved", ctypes.c_uint8)]
 
 
 class Record(ctypes.Structure):
@@ -109,6 +117,9 @@ def load(build_if_missing: bool = True):
     L.fc_run_read_hist.argtypes = [vp, _P(i64), _P(i64)]
     L.fc_run_read_edges.argtypes = [vp, _P(i64)]
     L.fc_run_read_flips.argtypes = [vp, _P(i64), _P(i64), _P(i64)]
+    L.fc_run_read_events.argtypes = [vp, i32, _P(Event), i64, _P(i64)]
+    L.fc_run_series_reset.argtypes = [vp]
+    L.fc_run_autocorr.argtypes = [vp, _P(i32), i32, _P(i64), _P(dbl)]
     L.fc_run_n_chains.argtypes = [vp]
     L.fc_run_n_chains.restype = i32
     L.fc_run_destroy.argtypes = [vp]

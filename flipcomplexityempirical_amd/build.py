@@ -12,7 +12,7 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libflipchain.so")
-SOURCES = ["fc_kernels.hip", "fc_capi.cpp", "fc_graph.cpp"]
+SOURCES = ["fc_kernels.hip", "fc_series.hip", "fc_capi.cpp", "fc_graph.cpp"]
 HEADERS = ["fc_internal.h", "fc_philox.h", os.path.join("..", "..", "include", "flipchain.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("FC_OFFLOAD_ARCH", "gfx950")

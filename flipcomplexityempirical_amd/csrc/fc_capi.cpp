@@ -46,6 +46,8 @@ struct fc_run {
     int64_t *d_num_flips = nullptr, *d_part_sum = nullptr, *d_last_flipped = nullptr;
     int32_t *d_popk = nullptr;
     int32_t wmax = 1;
+    fc_event *d_events = nullptr;
+    int64_t ev_cap = 0;
     fc_record *d_trace = nullptr;
     uint32_t *d_tape = nullptr;
     int64_t tape_draws = 0;
@@ -79,7 +81,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc, r->d_edge_since,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -292,9 +294,13 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         if (p->diag_mask & FC_DIAG_WAIT) {
             const uint32_t gid = p->chain_id_offset + (uint32_t)c;
             fc::Words4 w = fc::philox4x32_10(0u, 0u, gid, 2u, (uint32_t)p->seed, (uint32_t)(p->seed >> 32));
-            wait0 = (int64_t)std::ceil(std::log(1.0 - fc::u53(w.x0, w.x1)) / r->log1mp[nb]) - 1;
+            wait0 = fc::geom_from(fc::u53(w.x0, w.x1), r->log1mp[nb]);
         }
         s.wait_cur = wait0;
+        s.hit_time = (cut >= p->hit_lo && cut <= p->hit_hi) ? 0 : -1;
+        s.ser_t0 = 0;
+        s.ser_cut0 = cut;
+        s.ser_nb0 = nb;
         // yield #0 (the initial state) enters every per-yield sum
         s.sum_cut = cut;
         s.sum_nb = nb;
@@ -368,6 +374,13 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         HIP_TRY(hipMemset(r->d_last_flipped, 0, (size_t)n_chains * n * 8));
         HIP_TRY(hipMemcpy(r->d_part_sum, part_sum.data(), part_sum.size() * 8, hipMemcpyHostToDevice));
     }
+    if ((p->diag_mask & FC_DIAG_SERIES) && p->event_cap > 0) {
+        if (E > 65535) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: FC_DIAG_SERIES stores |cut| in 16 bits (E <= 65535)");
+        r->ev_cap = p->event_cap;
+        if ((rc = dalloc(&r->d_events, (size_t)n_chains * (size_t)p->event_cap))) return rc;
+    } else {
+        r->p.diag_mask &= ~FC_DIAG_SERIES;
+    }
     if (p->trace_chains > 0 && p->trace_cap > 0) {
         const int32_t tc = std::min(p->trace_chains, n_chains);
         r->p.trace_chains = tc;
@@ -439,6 +452,10 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.trace_cap = r->p.trace_cap;
     k.tape = r->d_tape;
     k.tape_draws = r->tape_draws;
+    k.events = r->d_events;
+    k.ev_cap = r->ev_cap;
+    k.hit_lo = r->p.hit_lo;
+    k.hit_hi = r->p.hit_hi;
     k.nsub = 1;
     if (const char *e = std::getenv("FC_NSUB")) k.nsub = std::atoi(e);
     k.hit_stop = 32;
@@ -524,6 +541,11 @@ int fc_run_read_stats(fc_run *r, fc_chain_stats *out) {
         o.nb = s.nb;
         o.last_flip = s.last_flip;
         o.stuck = s.stuck;
+        o.hit_time = s.hit_time;
+        o.events = s.ev_len;
+        o.series_t0 = s.ser_t0;
+        o.series_cut0 = s.ser_cut0;
+        o.series_nb0 = s.ser_nb0;
     }
     return FC_OK;
 }
@@ -579,6 +601,124 @@ int fc_run_trace_reset(fc_run *r) {
     for (auto &s : sc) s.trace_len = 0;
     HIP_TRY(hipMemcpy(r->d_sc, sc.data(), sc.size() * sizeof(sc[0]), hipMemcpyHostToDevice));
     return FC_OK;
+}
+
+int fc_run_read_events(fc_run *r, int32_t chain, fc_event *out, int64_t cap, int64_t *len) {
+    if (!r || !len || (cap > 0 && !out)) return fail(FC_ERR_ARG, "fc_run_read_events: null argument");
+    if (!r->d_events) return fail(FC_ERR_ARG, "fc_run_read_events: FC_DIAG_SERIES not enabled");
+    if (chain < 0 || chain >= r->n_chains) return fail(FC_ERR_ARG, "fc_run_read_events: chain out of range");
+    if (int rc = fc_run_sync(r)) return rc;
+    fc::ChainScalars s;
+    HIP_TRY(hipMemcpy(&s, r->d_sc + chain, sizeof s, hipMemcpyDeviceToHost));
+    const int64_t n = std::min<int64_t>({s.ev_len, r->ev_cap, cap});
+    if (n > 0)
+        HIP_TRY(hipMemcpy(out, r->d_events + (size_t)chain * r->ev_cap, (size_t)n * sizeof(fc_event),
+                          hipMemcpyDeviceToHost));
+    *len = s.ev_len;
+    return FC_OK;
+}
+
+int fc_run_series_reset(fc_run *r) {
+    if (!r) return fail(FC_ERR_ARG, "fc_run_series_reset: null run");
+    if (int rc = fc_run_sync(r)) return rc;
+    std::vector<fc::ChainScalars> sc(r->n_chains);
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    for (auto &s : sc) {
+        s.ev_len = 0;
+        s.ser_t0 = s.steps;
+        s.ser_cut0 = s.cut;
+        s.ser_nb0 = s.nb;
+    }
+    HIP_TRY(hipMemcpy(r->d_sc, sc.data(), sc.size() * sizeof(sc[0]), hipMemcpyHostToDevice));
+    return FC_OK;
+}
+
+int fc_run_autocorr(fc_run *r, const int32_t *lags, int32_t nlags, int64_t *lag_sums, double *acf) {
+    if (!r || !lags || nlags <= 0 || !lag_sums) return fail(FC_ERR_ARG, "fc_run_autocorr: null argument");
+    if (!r->d_events) return fail(FC_ERR_ARG, "fc_run_autocorr: FC_DIAG_SERIES not enabled");
+    for (int32_t j = 0; j < nlags; ++j)
+        if (lags[j] < 0) return fail(FC_ERR_ARG, "fc_run_autocorr: negative lag");
+    if (int rc = fc_run_sync(r)) return rc;
+    const int32_t C = r->n_chains;
+    std::vector<fc::ChainScalars> sc(C);
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    std::vector<int64_t> ev_len(C), t0(C), len(C);
+    std::vector<int32_t> cut0(C);
+    int64_t max_len = 0;
+    for (int32_t c = 0; c < C; ++c) {
+        if (sc[c].ev_len > r->ev_cap)
+            return fail(FC_ERR_ARG, "fc_run_autocorr: chain " + std::to_string(c) +
+                                        " overflowed event_cap; reset the series window more often");
+        ev_len[c] = sc[c].ev_len;
+        t0[c] = sc[c].ser_t0;
+        cut0[c] = sc[c].ser_cut0;
+        len[c] = sc[c].steps - sc[c].ser_t0 + 1;  // yields t0 .. steps
+        max_len = std::max(max_len, len[c]);
+    }
+    // lag 0 is always evaluated first: it yields the window totals Sx = H_0 and Sxx = P_0
+    std::vector<int32_t> lg(nlags + 1);
+    lg[0] = 0;
+    std::copy(lags, lags + nlags, lg.begin() + 1);
+    const int32_t nl = nlags + 1;
+    // device scratch: metadata + dense series for a batch of chains (<= 1 GiB)
+    const int64_t stride = (max_len + 7) & ~int64_t(7);
+    const int32_t batch = (int32_t)std::max<int64_t>(1, std::min<int64_t>({C, 65535, (int64_t(1) << 29) / stride}));
+    int64_t *d_meta = nullptr;
+    int32_t *d_cut0 = nullptr, *d_lags = nullptr;
+    uint16_t *d_x = nullptr;
+    unsigned long long *d_sums = nullptr;
+    auto cleanup = [&]() {
+        for (void *b : {(void *)d_meta, (void *)d_cut0, (void *)d_lags, (void *)d_x, (void *)d_sums})
+            if (b) (void)hipFree(b);
+    };
+    auto run = [&]() -> int {
+        int q;
+        if ((q = dalloc(&d_meta, (size_t)3 * C))) return q;
+        if ((q = dalloc(&d_cut0, (size_t)C))) return q;
+        if ((q = dalloc(&d_lags, (size_t)nl))) return q;
+        if ((q = dalloc(&d_x, (size_t)batch * stride))) return q;
+        if ((q = dalloc(&d_sums, (size_t)C * nl * 3))) return q;
+        HIP_TRY(hipMemcpy(d_meta, ev_len.data(), (size_t)C * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_meta + C, t0.data(), (size_t)C * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_meta + 2 * C, len.data(), (size_t)C * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_cut0, cut0.data(), (size_t)C * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_lags, lg.data(), (size_t)nl * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemsetAsync(d_sums, 0, (size_t)C * nl * 3 * 8, r->stream));
+        for (int32_t c0 = 0; c0 < C; c0 += batch) {
+            const int32_t nc = std::min(batch, C - c0);
+            int e = fc::launch_series_expand(r->d_events, r->ev_cap, d_meta, d_meta + C, d_cut0, d_meta + 2 * C, c0,
+                                             nc, stride, max_len, d_x, r->stream);
+            if (e) return fail(FC_ERR_HIP, std::string("series expand: ") + hipGetErrorString((hipError_t)e));
+            e = fc::launch_series_lagsums(d_x, d_meta + 2 * C, c0, nc, stride, max_len, d_lags, nl, d_sums,
+                                          r->stream);
+            if (e) return fail(FC_ERR_HIP, std::string("series lag sums: ") + hipGetErrorString((hipError_t)e));
+        }
+        std::vector<int64_t> sums((size_t)C * nl * 3);
+        HIP_TRY(hipMemcpyAsync(sums.data(), d_sums, sums.size() * 8, hipMemcpyDeviceToHost, r->stream));
+        HIP_TRY(hipStreamSynchronize(r->stream));
+        for (int32_t c = 0; c < C; ++c) {
+            const int64_t *s0 = &sums[(size_t)c * nl * 3];
+            const __int128 Sxx = s0[0], Sx = s0[1], T = len[c];
+            for (int32_t j = 0; j < nlags; ++j) {
+                const int64_t *s = s0 + 3 * (j + 1);
+                lag_sums[(size_t)c * nlags + j] = s[0];
+                if (!acf) continue;
+                const __int128 L = lags[j];
+                double v = 0.0;
+                if (L < T) {
+                    // T^2 * sum_{t < T-L} (x_t - m)(x_{t+L} - m), m = Sx / T, in exact integers
+                    const __int128 num = T * T * (__int128)s[0] - T * Sx * ((__int128)s[1] + s[2]) + (T - L) * Sx * Sx;
+                    const __int128 den = T * (T * Sxx - Sx * Sx);
+                    if (den != 0) v = (double)num / (double)den;
+                }
+                acf[(size_t)c * nlags + j] = v;
+            }
+        }
+        return FC_OK;
+    };
+    const int rc = run();
+    cleanup();
+    return rc;
 }
 
 int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist) {

@@ -58,12 +58,15 @@ struct ChainScalars {
     int64_t wait_cur;
     int64_t bfs_calls, bfs_levels;
     int64_t trace_len;
+    int64_t ev_len;         // FC_DIAG_SERIES events in the current window
+    int64_t hit_time;       // first yield with hit_lo <= cut <= hit_hi, -1: not yet
+    int64_t ser_t0;         // yield index starting the series window
     int32_t cut, nb;
     int32_t pops[kMaxK];
     int32_t ngamma[kMaxK];
     int32_t last_flip;
     int32_t stuck;
-    int32_t pad[2];
+    int32_t ser_cut0, ser_nb0;  // |cut|, |B| at ser_t0
 };
 
 // Kernel parameters (passed by value).
@@ -103,6 +106,9 @@ struct KParams {
     int32_t *popk;              // [n_chains * 32] district populations (k > 2)
     int32_t wmax;               // PAIR: foreign-district slots per node draw
     uint32_t wthresh;           // 2^32 mod wmax
+    fc_event *events;           // [n_chains * ev_cap] (FC_DIAG_SERIES)
+    int64_t ev_cap;
+    int32_t hit_lo, hit_hi;     // hitting-time window on |cut| (lo > hi: off)
     int32_t nsub;               // max draw rounds of 64 per batch (1, 2, 4)
     int32_t hit_stop;           // start another round only while fewer boundary hits than this
 };
@@ -110,5 +116,15 @@ struct KParams {
 // Launch wrappers (fc_kernels.hip).  Return a hipError_t as int.
 int launch_flip_k2(const KParams &p, int ring_max, void *stream);
 int launch_init_fcnt(const KParams &p, int ring_max, void *stream);
+
+// Series diagnostics (fc_series.hip): expand the event logs of chains [c0, c0 + nc) into
+// dense |cut| series x[(c - c0) * stride + t], t < len[c], then accumulate per lag
+// P = sum x_t x_{t+L}, H = sum_{t < len-L} x_t, G = sum_{t >= L} x_t into sums[c][lag][3].
+int launch_series_expand(const fc_event *events, int64_t ev_cap, const int64_t *ev_len, const int64_t *t0,
+                         const int32_t *cut0, const int64_t *len, int32_t c0, int32_t nc, int64_t stride,
+                         int64_t max_len, uint16_t *x, void *stream);
+int launch_series_lagsums(const uint16_t *x, const int64_t *len, int32_t c0, int32_t nc, int64_t stride,
+                          int64_t max_len, const int32_t *lags, int32_t nlags, unsigned long long *sums,
+                          void *stream);
 
 }  // namespace fc

@@ -172,6 +172,7 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     int64_t steps = scp->steps;  // index of the current yield
     int64_t bfs_calls = scp->bfs_calls, bfs_levels = scp->bfs_levels;
     int64_t trace_len = scp->trace_len;
+    int64_t ev_len = scp->ev_len, hit_time = scp->hit_time;
     int cut = scp->cut, nb = scp->nb;
     int pops0 = scp->pops[0], pops1 = scp->pops[1];
     int ng0 = scp->ngamma[0], ng1 = scp->ngamma[1];
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
                 g = philox4x32_10((uint32_t)d, (uint32_t)(d >> 32), chain_gid, 1u, p.seed_lo, p.seed_hi);
             }
             const double U = u53(g.x0, g.x1);
-            my_wait = (int64_t)ceil(log(1.0 - U) / p.log1mp[nb_after]) - 1;
+            my_wait = geom_from(U, p.log1mp[nb_after]);
         }
         if (is_acc) {
             acc_cut += (int64_t)cut_after * run_len;
@@ -517,8 +518,26 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
             acc_nb2 += (int64_t)nb0 * nb0 * r0;
             acc_wait += wait_cur * r0;
         }
+        const int64_t t_acc = steps0 + __popcll(VSM & bits_below(lane + 1));  // yield index of this slot
+        if ((p.diag & FC_DIAG_SERIES) && ACCM) {
+            const int64_t idx = ev_len + __popcll(ACCM & bits_below(lane));
+            if (is_acc && idx < p.ev_cap) {
+                fc_event ev;
+                ev.t = t_acc;
+                ev.v = (uint16_t)v;
+                ev.cut = (uint16_t)cut_after;
+                ev.nb = (uint16_t)nb_after;
+                ev.target = (uint8_t)tgt;
+                ev.reserved = 0;
+                p.events[(size_t)c * p.ev_cap + idx] = ev;
+            }
+            ev_len += __popcll(ACCM);
+        }
+        if (hit_time < 0 && ACCM) {
+            const uint64_t hm = __ballot(is_acc && cut_after >= p.hit_lo && cut_after <= p.hit_hi);
+            if (hm) hit_time = (int64_t)__shfl((long long)t_acc, __builtin_ctzll(hm));
+        }
         if (p.diag & (FC_DIAG_HIST | FC_DIAG_FLIPS | FC_DIAG_EDGES)) {
-            const int64_t t_acc = steps0 + __popcll(VSM & bits_below(lane + 1));  // yield index of this slot
             if (p.diag & FC_DIAG_HIST) {
                 if (is_acc) {
                     atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
@@ -620,6 +639,8 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
         scp->bfs_calls = bfs_calls;
         scp->bfs_levels = bfs_levels;
         scp->trace_len = trace_len;
+        scp->ev_len = ev_len;
+        scp->hit_time = hit_time;
         scp->sum_cut += acc_cut;
         scp->sum_nb += acc_nb;
         scp->sum_wait += acc_wait;

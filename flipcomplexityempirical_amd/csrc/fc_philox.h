@@ -6,6 +6,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <cmath>
+
 #if defined(__HIPCC__) || defined(__HIP__)
 #define FC_HD __host__ __device__ __forceinline__
 #else
@@ -48,5 +50,15 @@ FC_HD Words4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, u
 FC_HD uint64_t mant53(uint32_t a, uint32_t b) { return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6); }
 
 FC_HD double u53(uint32_t a, uint32_t b) { return (double)mant53(a, b) * (1.0 / 9007199254740992.0); }
+
+// geom_wait (grid_chain_sec11.py:147-148) by numpy's legacy inversion, ceil(log(1-U)/log(1-p)) - 1,
+// saturated at 2^62 where log(1-p) rounds to 0 (|B| / (N^k - 1) below 2^-53, e.g. k >= 5 on 10^4
+// nodes) -- the reference's float pipeline has no defined value there.
+constexpr double kWaitCap = 4611686018427387904.0;  // 2^62
+FC_HD int64_t geom_from(double U, double log1mp) {
+    const double q = log(1.0 - U) / log1mp;
+    if (!(fabs(q) < kWaitCap)) return (int64_t)kWaitCap;
+    return (int64_t)ceil(q) - 1;
+}
 
 }  // namespace fc

@@ -22,6 +22,8 @@ _P = ctypes.POINTER
 STAT_FIELDS = [f for f, _ in _lib.ChainStats._fields_]
 RECORD_DTYPE = np.dtype([("draw", "<i8"), ("v", "<i4"), ("flags", "<i4"), ("cut", "<i4"),
                          ("nb", "<i4"), ("wait", "<i8")])
+EVENT_DTYPE = np.dtype([("t", "<i8"), ("v", "<u2"), ("cut", "<u2"), ("nb", "<u2"), ("target", "u1"),
+                        ("reserved", "u1")])
 
 
 def _p(arr, ct):
@@ -99,6 +101,9 @@ class RunConfig:
     labels: Sequence[int] = (-1, 1)
     proposal: int = _lib.FC_PROPOSE_BI_SIGN
     wmax: int = 0
+    hit_lo: int = 1          # hitting-time window on |cut| (hit_lo > hit_hi: off)
+    hit_hi: int = 0
+    event_cap: int = 0       # FC_DIAG_SERIES events kept per chain per window
 
 
 class FlipRun:
@@ -118,7 +123,8 @@ class FlipRun:
         self._init = np.ascontiguousarray(a)
         if self._init.shape[1] != graph.n:
             raise ValueError("init_assign must have one entry per node")
-        self._labels = np.ascontiguousarray(cfg.labels, dtype=np.int32)
+        labels = list(cfg.labels) if len(cfg.labels) == cfg.k else list(range(cfg.k))
+        self._labels = np.ascontiguousarray(labels, dtype=np.int32)
         self._log1mp = np.ascontiguousarray(log1mp if log1mp is not None else log1mp_table(graph.n, cfg.k),
                                             dtype=np.float64)
         self._bases = None if bases is None else np.ascontiguousarray(bases, dtype=np.float64)
@@ -129,7 +135,8 @@ class FlipRun:
                           chain_id_offset=int(cfg.chain_id_offset), diag_mask=int(cfg.diag_mask),
                           flags=int(cfg.flags), device=int(cfg.device), trace_chains=int(cfg.trace_chains),
                           trace_cap=int(cfg.trace_cap), labels=_p(self._labels, ctypes.c_int32),
-                          log1mp=_p(self._log1mp, ctypes.c_double))
+                          log1mp=_p(self._log1mp, ctypes.c_double), hit_lo=int(cfg.hit_lo),
+                          hit_hi=int(cfg.hit_hi), event_cap=int(cfg.event_cap))
         h = ctypes.c_void_p()
         check(L.fc_run_create(graph.handle, ctypes.byref(prm), self.n_chains, _p(self._init, ctypes.c_int8),
                               _p(self._bases, ctypes.c_double), ctypes.byref(h)), "fc_run_create")
@@ -218,6 +225,41 @@ class FlipRun:
         check(_lib.load().fc_run_read_flips(self.handle, _p(nf, ctypes.c_int64), _p(ps, ctypes.c_int64),
                                             _p(lf, ctypes.c_int64)))
         return nf, ps, lf
+
+    # ---- series diagnostics (FC_DIAG_SERIES) ------------------------------------------
+    def events(self, chain: int = 0) -> np.ndarray:
+        """Accepted flips of ``chain`` in the current series window (``fc_event``)."""
+        cap = int(self.cfg.event_cap)
+        out = np.zeros(cap, dtype=EVENT_DTYPE)
+        n = ctypes.c_int64(0)
+        check(_lib.load().fc_run_read_events(self.handle, chain, ctypes.cast(out.ctypes.data, _P(_lib.Event)),
+                                             cap, ctypes.byref(n)), "fc_run_read_events")
+        if n.value > cap:
+            raise OverflowError(f"event capacity {cap} exceeded ({n.value} events)")
+        return out[:n.value]
+
+    def series_reset(self):
+        check(_lib.load().fc_run_series_reset(self.handle), "fc_run_series_reset")
+
+    def cut_series(self, chain: int = 0) -> np.ndarray:
+        """|cut| at every yield of the window -- the reference's ``rce`` list
+        (``grid_chain_sec11.py:367``) -- expanded on the host from the event log."""
+        st = self.stats()
+        t0, x0, T = int(st["series_t0"][chain]), int(st["series_cut0"][chain]), int(st["steps"][chain])
+        ev = self.events(chain)
+        bounds = np.concatenate([[t0], ev["t"], [T + 1]]).astype(np.int64)
+        vals = np.concatenate([[x0], ev["cut"].astype(np.int64)])
+        return np.repeat(vals, np.diff(bounds))
+
+    def autocorr(self, lags: Sequence[int]):
+        """Device autocorrelation of the |cut| series over the window: ``(lag_sums, acf)``,
+        each ``[n_chains, len(lags)]`` (``fc_run_autocorr``)."""
+        lg = np.ascontiguousarray(lags, dtype=np.int32)
+        sums = np.zeros((self.n_chains, lg.size), dtype=np.int64)
+        acf = np.zeros((self.n_chains, lg.size), dtype=np.float64)
+        check(_lib.load().fc_run_autocorr(self.handle, _p(lg, ctypes.c_int32), int(lg.size),
+                                          _p(sums, ctypes.c_int64), _p(acf, ctypes.c_double)), "fc_run_autocorr")
+        return sums, acf
 
     def close(self):
         if getattr(self, "handle", None):

@@ -50,6 +50,9 @@ extern "C" {
 #define FC_DIAG_HIST 0x2u        /* per-chain histograms of |cut| and |B| over yields        */
 #define FC_DIAG_EDGES 0x4u       /* per-edge cut_times, :383-384                             */
 #define FC_DIAG_FLIPS 0x8u       /* per-node num_flips / part_sum / last_flipped, :396-400   */
+#define FC_DIAG_SERIES 0x10u     /* per-chain log of accepted flips (fc_event): the rce / rbn
+                                    series of :367-369 in run-length form; feeds
+                                    fc_run_autocorr and the slope / angle series (:371-392)  */
 
 /* fc_params.flags */
 #define FC_FLAG_FORCE_BFS 0x1u   /* resolve every multi-run contiguity case by device BFS   */
@@ -84,6 +87,9 @@ typedef struct fc_params {
     const int32_t *labels;     /* [k] reference district labels (e.g. -1, 1); NULL = 0..k-1 */
     const double *log1mp;      /* [n+1] log(1 - b/(N^k - 1)); NULL = computed in double     */
     int32_t wmax;              /* PAIR: district slots per node draw (<= 0: min(max deg, k-1)) */
+    int32_t hit_lo, hit_hi;    /* hitting time: first yield with hit_lo <= |cut| <= hit_hi
+                                  (hit_lo > hit_hi: off)                                     */
+    int64_t event_cap;         /* FC_DIAG_SERIES: events kept per chain per series window    */
 } fc_params;
 
 /* Per-chain statistics.  "Yields" are the states a `for part in exp_chain` loop sees:
@@ -107,7 +113,23 @@ typedef struct fc_chain_stats {
     int32_t nb;           /* current |b_nodes|                                             */
     int32_t last_flip;    /* node flipped to create the current state (-1: initial)       */
     int32_t stuck;        /* a launch hit max_draws before finishing its steps            */
+    int64_t hit_time;     /* first yield index with |cut| in [hit_lo, hit_hi], -1: not yet  */
+    int64_t events;       /* accepted flips in the current series window (may exceed cap) */
+    int64_t series_t0;    /* yield index at which the series window starts                */
+    int32_t series_cut0;  /* |cut| of that yield                                           */
+    int32_t series_nb0;   /* |B| of that yield                                             */
 } fc_chain_stats;
+
+/* One accepted flip (FC_DIAG_SERIES): yield t is the first state with a[v] = target;
+ * |cut| and |B| hold from yield t until the next event's t (16 B). */
+typedef struct fc_event {
+    int64_t t;
+    uint16_t v;
+    uint16_t cut;
+    uint16_t nb;
+    uint8_t target;
+    uint8_t reserved;
+} fc_event;
 
 /* One record per proposal (trace mode), identical in layout to the oracle's. */
 typedef struct fc_record {
@@ -163,6 +185,17 @@ int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist);      /* [c
 int fc_run_read_edges(fc_run *r, int64_t *cut_times);                     /* [c*E], finalised     */
 /* num_flips / part_sum / last_flipped [c*n], finalised as grid_chain_sec11.py:416-418. */
 int fc_run_read_flips(fc_run *r, int64_t *num_flips, int64_t *part_sum, int64_t *last_flipped);
+/* ---- series diagnostics (FC_DIAG_SERIES): the per-yield lists rce / rbn (:367-369) ----- */
+/* Events of one chain's current window (*len = events recorded, may exceed cap). */
+int fc_run_read_events(fc_run *r, int32_t chain, fc_event *out, int64_t cap, int64_t *len);
+/* Start a new window at the current yield (events dropped; hit_time is kept). */
+int fc_run_series_reset(fc_run *r);
+/* Autocorrelation of the |cut| series over the window's yields t0..steps, on the device:
+ * lag_sums[c * nlags + j] = sum_t x_t x_{t + lags[j]} (exact int64), and, if acf != NULL,
+ * acf[c * nlags + j] = sum_t (x_t - m)(x_{t+L} - m) / sum_t (x_t - m)^2 with m the window
+ * mean (the biased sample ACF, statsmodels' acf default), formed on the host from exact
+ * integer sums.  FC_ERR_ARG if a chain's event log overflowed event_cap. */
+int fc_run_autocorr(fc_run *r, const int32_t *lags, int32_t nlags, int64_t *lag_sums, double *acf);
 int32_t fc_run_n_chains(const fc_run *r);
 void fc_run_destroy(fc_run *r);
 

@@ -155,7 +155,9 @@ static int64_t geom_wait(const fr_params *p, int64_t d, uint32_t purpose, int32_
     uint32_t w[4];
     draw_words(p, d, purpose, w);
     double U = u53(w[0], w[1]);
-    return (int64_t)ceil(log(1.0 - U) / p->log1mp[nb]) - 1;
+    double q = log(1.0 - U) / p->log1mp[nb];
+    if (!(fabs(q) < 4611686018427387904.0)) return (int64_t)4611686018427387904LL; /* saturate: 2^62 */
+    return (int64_t)ceil(q) - 1;
 }
 
 /* One driver-loop iteration (grid_chain_sec11.py:366-402) for the yielded state. */

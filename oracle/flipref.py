@@ -374,7 +374,11 @@ class GcFaithfulChain:
         w = self._words(d, purpose)
         U = u53(w[0], w[1])
         nb = len(self.state["b_nodes"])
-        return int(math.ceil(math.log(1.0 - U) / self.log1mp[nb])) - 1
+        l1 = self.log1mp[nb]
+        q = math.log(1.0 - U) / l1 if l1 != 0.0 else -math.inf
+        if not abs(q) < 2.0 ** 62:
+            return 1 << 62  # saturated, as the C restatement
+        return int(math.ceil(q)) - 1
 
     def _yield(self):
         s = self.state
@@ -447,3 +451,64 @@ class GcFaithfulChain:
     def assignment_ids(self):
         lut = {lab: i for i, lab in enumerate(self.labels)}
         return np.asarray([lut[self.state.assignment[nd]] for nd in self.spec.nodes], dtype=np.int8)
+
+
+# --------------------------------------------------------------------------------------
+# Series diagnostics restated from a proposal trace (checker for FC_DIAG_SERIES).
+# The reference driver keeps the per-yield lists rce / rbn (grid_chain_sec11.py:367-369);
+# C4 asks for their autocorrelation and a hitting time of a target |cut|.
+# --------------------------------------------------------------------------------------
+def yield_series(trace: np.ndarray, x0: int, field: str = "cut") -> np.ndarray:
+    """Per-yield values (yield 0 = the initial state with value ``x0``; one yield per
+    valid proposal) from an oracle/device proposal trace."""
+    valid = (trace["flags"] & FLAG_VALID) != 0
+    return np.concatenate([[x0], trace[field][valid]]).astype(np.int64)
+
+
+def events_from_trace(trace: np.ndarray) -> np.ndarray:
+    """(t, v, cut, nb, target) of every accepted flip: t = yield index it creates."""
+    valid = (trace["flags"] & FLAG_VALID) != 0
+    t = np.cumsum(valid.astype(np.int64))
+    acc = (trace["flags"] & FLAG_ACCEPTED) != 0
+    return np.stack([t[acc], trace["v"][acc], trace["cut"][acc], trace["nb"][acc],
+                     (trace["flags"][acc] >> 8) & 0xFF], axis=1).astype(np.int64)
+
+
+def hitting_time(series: np.ndarray, lo: int, hi: int) -> int:
+    hit = np.nonzero((series >= lo) & (series <= hi))[0]
+    return int(hit[0]) if hit.size else -1
+
+
+def acf_exact(x: np.ndarray, lags) -> tuple:
+    """Biased sample ACF (statsmodels ``acf`` default) of an integer series, formed exactly
+    as ``fc_run_autocorr`` does: integer lag sums, then one rounding of the exact rational
+    T^2 sum (x_t - m)(x_{t+L} - m) / (T^2 sum (x_t - m)^2) to double.  Returns
+    ``(lag_sums, acf)``."""
+    xs = [int(v) for v in x]
+    T = len(xs)
+    Sx = sum(xs)
+    Sxx = sum(v * v for v in xs)
+    sums, out = [], []
+    for L in lags:
+        L = int(L)
+        if L >= T:
+            sums.append(0)
+            out.append(0.0)
+            continue
+        P = sum(xs[t] * xs[t + L] for t in range(T - L))
+        H = sum(xs[:T - L])
+        G = sum(xs[L:])
+        num = T * T * P - T * Sx * (H + G) + (T - L) * Sx * Sx
+        den = T * (T * Sxx - Sx * Sx)
+        sums.append(P)
+        out.append(float(num) / float(den) if den else 0.0)
+    return np.asarray(sums, dtype=np.int64), np.asarray(out, dtype=np.float64)
+
+
+def acf_float(x: np.ndarray, lags) -> np.ndarray:
+    """The same ACF in plain float64 numpy (tolerance cross-check)."""
+    x = np.asarray(x, dtype=np.float64)
+    d = x - x.mean()
+    den = float(np.dot(d, d))
+    return np.asarray([float(np.dot(d[:len(d) - L], d[L:])) / den if L < len(d) and den else 0.0
+                       for L in lags])

@@ -1,0 +1,121 @@
+"""GPU parity of the series diagnostics (FC_DIAG_SERIES event log, hitting time, device
+autocorrelation) against the oracle's proposal trace.
+
+The reference driver builds the per-yield lists rce / rbn (grid_chain_sec11.py:367-369);
+BASELINE config C4 asks for the autocorrelation of the cut trace and a hitting time of a
+target cut count.  Integer outputs are bit-exact; the ACF is formed from exact integer lag
+sums and is compared bit-exactly with the same rational in Python, and within 1e-9 with a
+plain float64 ACF.
+"""
+import numpy as np
+import pytest
+
+from flipcomplexityempirical_amd import graphs as G
+from flipcomplexityempirical_amd import _lib
+from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+from oracle.flipref import acf_exact, acf_float, events_from_trace, hitting_time, yield_series
+
+pytestmark = pytest.mark.gpu
+
+DIAG = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_SERIES
+LAGS = [1, 2, 3, 7, 16, 100, 1000, 4097, 5000]
+
+
+def _setup(spec, k, plan, bases, *, pct, hit, event_cap=200000, proposal=None, seed=31):
+    fg = FlipGraph(spec)
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
+    labels = [-1, 1] if k == 2 else list(range(k))
+    a0 = spec.assignment_array(plan, labels)
+    inits = np.stack([a0] * len(bases))
+    cfg = RunConfig(k=k, labels=tuple(labels) if k == 2 else tuple(range(k)),
+                    proposal=(_lib.FC_PROPOSE_BI_SIGN if k == 2 else _lib.FC_PROPOSE_PAIR) if proposal is None else proposal,
+                    seed=seed, pop_lo=lo, pop_hi=hi, diag_mask=DIAG, trace_chains=len(bases), trace_cap=400000,
+                    hit_lo=hit[0], hit_hi=hit[1], event_cap=event_cap)
+    return FlipRun(fg, inits, cfg, bases=np.asarray(bases)), inits
+
+
+def _oracle_trace(cref, spec, k, init, base, c, steps, pct, seed=31):
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
+    r = cref.run(spec, init, base=float(base), pop_lo=lo, pop_hi=hi, seed=seed, chain_id=c, n_steps=steps, k=k,
+                 labels=[-1, 1] if k == 2 else list(range(k)), log1mp=G.log1mp_table(spec.n, k), trace_cap=500000,
+                 proposal=0 if k == 2 else 1)
+    return r["trace"]
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_sec11_events_hitting_autocorr(gpu, cref, sec11, chunks):
+    bases = [0.1, 1 / G.SEC11_MU, 1.0, G.SEC11_MU, 10.0, 0.5]
+    steps = 6000
+    x0 = G.cut_and_boundary(sec11, sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1]))[0]
+    hit = (x0 + 20, 10 ** 6)
+    run, inits = _setup(sec11, 2, G.sec11_plan(0, sec11.nodes), bases, pct=0.1, hit=hit)
+    for i in range(chunks):
+        run.steps(steps // chunks)
+    st = run.stats()
+    sums, acf = run.autocorr(LAGS)
+    for c, b in enumerate(bases):
+        tr = _oracle_trace(cref, sec11, 2, inits[c], b, c, steps, 0.1)
+        ev = run.events(c)
+        exp = events_from_trace(tr)
+        assert len(ev) == len(exp) == st["events"][c]
+        got = np.stack([ev["t"], ev["v"], ev["cut"], ev["nb"], ev["target"]], axis=1).astype(np.int64)
+        assert np.array_equal(got, exp)
+        x = yield_series(tr, x0)
+        assert np.array_equal(run.cut_series(c), x)
+        assert st["hit_time"][c] == hitting_time(x, *hit)
+        es, ea = acf_exact(x, LAGS)
+        assert np.array_equal(sums[c], es)
+        assert np.array_equal(acf[c], ea)
+        np.testing.assert_allclose(acf[c], acf_float(x, LAGS), rtol=0, atol=1e-9)
+
+
+def test_series_window_reset(gpu, cref, sec11):
+    """A window started mid-run covers yields t0..steps only."""
+    bases = [0.8, 2.0]
+    run, inits = _setup(sec11, 2, G.sec11_plan(1, sec11.nodes), bases, pct=0.1, hit=(1, 0))
+    run.steps(2000)
+    run.series_reset()
+    run.steps(3000)
+    st = run.stats()
+    x0 = G.cut_and_boundary(sec11, inits[0])[0]
+    sums, acf = run.autocorr([1, 10, 250])
+    for c, b in enumerate(bases):
+        x = yield_series(_oracle_trace(cref, sec11, 2, inits[c], b, c, 5000, 0.1), x0)
+        assert st["series_t0"][c] == 2000 and st["series_cut0"][c] == x[2000]
+        assert st["hit_time"][c] == -1
+        w = x[2000:]
+        assert np.array_equal(run.cut_series(c), w)
+        es, ea = acf_exact(w, [1, 10, 250])
+        assert np.array_equal(sums[c], es) and np.array_equal(acf[c], ea)
+
+
+def test_c4_triangular_k8_series(gpu, cref):
+    spec = G.triangular_graph(30, 58)
+    k = 8
+    plan = G.strip_plan(spec, k)
+    x0 = G.cut_and_boundary(spec, spec.assignment_array(plan, list(range(k))))[0]
+    bases = [0.5, 1.0, 2.0, 4.0]
+    hit = (0, x0 - 10)
+    run, inits = _setup(spec, k, plan, bases, pct=0.1, hit=hit)
+    run.steps(4000)
+    st = run.stats()
+    sums, acf = run.autocorr(LAGS)
+    for c, b in enumerate(bases):
+        tr = _oracle_trace(cref, spec, k, inits[c], b, c, 4000, 0.1)
+        x = yield_series(tr, x0)
+        got = run.events(c)
+        assert np.array_equal(np.stack([got["t"], got["v"], got["cut"], got["nb"], got["target"]], 1).astype(np.int64),
+                              events_from_trace(tr))
+        assert st["hit_time"][c] == hitting_time(x, *hit)
+        es, ea = acf_exact(x, LAGS)
+        assert np.array_equal(sums[c], es) and np.array_equal(acf[c], ea)
+
+
+def test_event_overflow_is_reported(gpu, sec11):
+    run, _ = _setup(sec11, 2, G.sec11_plan(0, sec11.nodes), [1.0], pct=0.1, hit=(1, 0), event_cap=100)
+    run.steps(3000)
+    assert run.stats()["events"][0] > 100
+    with pytest.raises(ValueError):
+        run.autocorr([1])
+    with pytest.raises(OverflowError):
+        run.events(0)
