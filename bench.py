@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Headline benchmark: flip proposals/s on the 40x40 sec11 grid, k = 2 (BASELINE.json).
 
+``--workload`` selects another BASELINE config for side measurements (never the headline
+line): c3 (sec11, k=4 pair proposals, 8192 chains/GPU), c4 (triangular 100x198, k=8),
+c5 (Delaunay 10k nodes, k=18).  The default, c2, is the line the driver records.
+
 Workload (BASELINE config C2, the largest single-GPU configuration of the metric):
 the exact sec11 graph of ``grid_chain_sec11.py:186-260`` (N = 1596, E = 3116), 4096
 independent chains per GPU, chain c (global id g) with base ``bases[g % 10]``
@@ -34,6 +38,75 @@ LDS_PEAK_GBS = 150000.0         # MI355X_MICROARCH.md §LDS: ~150 TB/s ds_read_b
 # accepted proposal W = 1 + 8 + 4*(deg+1) + 4 with deg = 4, L = 4 (sec11 interior).
 R_BYTES = 2 + 1 + 8 + 5 * 4 + 5 * 4 + 8      # 59
 W_BYTES = 1 + 8 + 4 * (4 + 1) + 4            # 33
+MU_TRI = 4.150797226                         # connective constant of the triangular lattice
+
+
+def r_bytes(deg: float, ring_extra: float) -> float:
+    return 2 + 1 + 8 + 5 * deg + 5 * ring_extra + 8
+
+
+def w_bytes(deg: float) -> float:
+    return 1 + 8 + 4 * (deg + 1) + 4
+
+
+class Workload:
+    """One BASELINE config: graph, start plan and base of global chain g, bounds."""
+
+    def __init__(self, name: str):
+        from flipcomplexityempirical_amd import graphs as G
+        from flipcomplexityempirical_amd import _lib
+        self.name = name
+        if name == "c2":
+            self.spec = G.sec11_graph()
+            self.k, self.pct, self.proposal, self.labels = 2, 0.1, _lib.FC_PROPOSE_BI_SIGN, [-1, 1]
+            self.bases = list(G.SEC11_BASES)
+            self._plans = [self.spec.assignment_array(G.sec11_plan(al, self.spec.nodes), [-1, 1]) for al in range(3)]
+            self.plan_of = lambda g: (g // 10) % 3
+            self.chains = 4096
+            self.R, self.W = R_BYTES, W_BYTES
+            self.desc = ("C2: sec11 40x40 grid (N=1596, E=3116), k=2, 4096 chains/GPU, base bases[g%10], "
+                         "alignment (g//10)%3, pop tol 0.1, seed 0x5EED0002")
+        elif name == "c3":
+            self.spec = G.sec11_graph()
+            self.k, self.pct, self.proposal, self.labels = 4, 0.05, _lib.FC_PROPOSE_PAIR, [0, 1, 2, 3]
+            self.bases = [G.SEC11_MU]
+            self._plans = [self.spec.assignment_array(G.quadrant_plan(self.spec.nodes), self.labels)]
+            self.plan_of = lambda g: 0
+            self.chains = 8192
+            self.R, self.W = R_BYTES + 8, W_BYTES   # k pops compared: two more int32 reads
+            self.desc = "C3: sec11 40x40, k=4 quadrant plan, pair proposals, pop tol 0.05, base mu, 8192 chains/GPU"
+        elif name == "c4":
+            self.spec = G.triangular_graph(100, 198)
+            self.k, self.pct, self.proposal = 8, 0.1, _lib.FC_PROPOSE_PAIR
+            self.labels = list(range(8))
+            self.bases = [1 / MU_TRI, 1.0, MU_TRI]
+            self._plans = [self.spec.assignment_array(G.strip_plan(self.spec, 8), self.labels)]
+            self.plan_of = lambda g: 0
+            self.chains = 2048
+            self.R, self.W = r_bytes(6, 0), w_bytes(6)
+            self.desc = (f"C4: triangular lattice 100x198 (N={self.spec.n}), k=8 vertical strips, pair proposals, "
+                         "pop tol 0.1, base in {1/mu_tri, 1, mu_tri}, 2048 chains/GPU")
+        elif name == "c5":
+            self.spec = G.delaunay_graph(10000, seed=0)
+            self.k, self.pct, self.proposal = 18, 0.1, _lib.FC_PROPOSE_PAIR
+            self.labels = list(range(18))
+            self.bases = [0.5, 1.0, 2.0]
+            self._plans = [self.spec.assignment_array(G.bisection_plan(self.spec, 18), self.labels)]
+            self.plan_of = lambda g: 0
+            self.chains = 2048
+            d = float(self.spec.degree().mean())
+            self.R, self.W = r_bytes(d, 0), w_bytes(d)
+            self.desc = ("C5: Delaunay dual of 10^4 uniform points (E=%d), lognormal pops, k=18 bisection plan, "
+                         "pair proposals, pop tol 0.1, base in {0.5, 1, 2}, 2048 chains/GPU" % self.spec.n_edges)
+        else:
+            raise ValueError(f"unknown workload {name}")
+        self.seed = SEED + {"c2": 0, "c3": 1, "c4": 2, "c5": 3}[name]
+
+    def base_of(self, g):
+        return self.bases[g % len(self.bases)]
+
+    def init_of(self, g):
+        return self._plans[self.plan_of(g)]
 
 
 def _dist():
@@ -52,15 +125,17 @@ def _dist():
 
 def _cpu_worker(args):
     """One chain of the same workload on the gerrychain-faithful Python port."""
-    gid, seconds = args
+    gid, seconds, wname = args
     sys.path.insert(0, ROOT)
     from flipcomplexityempirical_amd import graphs as G
     from oracle.flipref import GcFaithfulChain
-    spec = G.sec11_graph()
-    plan = G.sec11_plan((gid // 10) % 3, spec.nodes)
-    (lo, hi), _ = G.population_bounds(spec.n, 2, 0.1)
-    ch = GcFaithfulChain(spec, plan, base=G.SEC11_BASES[gid % 10], pop_bounds=(lo, hi), seed=SEED,
-                         chain_id=gid, log1mp=G.log1mp_table(spec.n, 2))
+    w = Workload(wname)
+    spec = w.spec
+    a = w.init_of(gid)
+    plan = {spec.nodes[i]: w.labels[int(a[i])] for i in range(spec.n)}
+    (lo, hi), _ = G.population_bounds(int(spec.pop.sum()), w.k, w.pct)
+    ch = GcFaithfulChain(spec, plan, base=w.base_of(gid), pop_bounds=(lo, hi), seed=w.seed,
+                         chain_id=gid, log1mp=G.log1mp_table(spec.n, w.k), pair=w.k > 2)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         for _ in range(20):
@@ -69,10 +144,10 @@ def _cpu_worker(args):
     return ch.stats["proposals"], ch.stats["steps"], dt
 
 
-def cpu_baseline(seconds: float, cores: int):
+def cpu_baseline(seconds: float, cores: int, wname: str = "c2"):
     from concurrent.futures import ProcessPoolExecutor
     with ProcessPoolExecutor(max_workers=cores) as ex:
-        res = list(ex.map(_cpu_worker, [(g, seconds) for g in range(cores)]))
+        res = list(ex.map(_cpu_worker, [(g, seconds, wname) for g in range(cores)]))
     props = sum(r[0] for r in res)
     wall = max(r[2] for r in res)
     return {"value": props / wall, "unit": "proposals/s", "cores": cores, "kind": "port",
@@ -81,19 +156,19 @@ def cpu_baseline(seconds: float, cores: int):
                       f"{seconds:.0f} s each from the start plans; {props} proposals"}
 
 
-def c_oracle_rate(seconds: float):
+def c_oracle_rate(seconds: float, wname: str = "c2"):
     """Single-core rate of the plain-C oracle on the same workload (extra, informational)."""
     from flipcomplexityempirical_amd import graphs as G
     from oracle.flipref import CRef
-    spec = G.sec11_graph()
+    w = Workload(wname)
+    spec = w.spec
     cref = CRef()
-    _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
-    l1 = G.log1mp_table(spec.n, 2)
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), w.k, w.pct)
+    l1 = G.log1mp_table(spec.n, w.k)
     props, t0, g = 0, time.perf_counter(), 0
     while time.perf_counter() - t0 < seconds:
-        a0 = spec.assignment_array(G.sec11_plan((g // 10) % 3, spec.nodes), [-1, 1])
-        r = cref.run(spec, a0, base=G.SEC11_BASES[g % 10], pop_lo=lo, pop_hi=hi, seed=SEED, chain_id=g,
-                     n_steps=20000, log1mp=l1)
+        r = cref.run(spec, w.init_of(g), base=w.base_of(g), pop_lo=lo, pop_hi=hi, seed=w.seed, chain_id=g,
+                     n_steps=20000, log1mp=l1, k=w.k, labels=w.labels, proposal=w.proposal)
         props += r["stats"]["proposals"]
         g += 1
     return props / (time.perf_counter() - t0)
@@ -105,7 +180,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chain-steps", type=int, default=10000)
-    ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
+    ap.add_argument("--chains", type=int, default=0, help="chains per GPU (0: the workload's)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -115,17 +191,18 @@ def main():
     from flipcomplexityempirical_amd import graphs as G
     from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
 
-    spec = G.sec11_graph()
+    W = Workload(args.workload)
+    spec = W.spec
     fg = FlipGraph(spec)
     from flipcomplexityempirical_amd import distributed as D
-    C = args.chains
+    C = args.chains or W.chains
     off, cnt = D.shard(C * world, world, rank)          # weak scaling: C chains per GPU
     gids = np.arange(off, off + cnt)
-    plans = [spec.assignment_array(G.sec11_plan(al, spec.nodes), [-1, 1]) for al in range(3)]
-    inits = np.stack([plans[(g // 10) % 3] for g in gids])
-    bases = np.asarray([G.SEC11_BASES[g % 10] for g in gids])
-    _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
-    cfg = RunConfig(seed=SEED, pop_lo=lo, pop_hi=hi, chain_id_offset=int(off), device=local_rank)
+    inits = np.stack([W.init_of(int(g)) for g in gids])
+    bases = np.asarray([W.base_of(int(g)) for g in gids])
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), W.k, W.pct)
+    cfg = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
+                    chain_id_offset=int(off), device=local_rank)
     run = FlipRun(fg, inits, cfg, bases=bases)
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
@@ -162,7 +239,8 @@ def main():
     if dist is not None and dist.get_backend() == "nccl":
         dev = torch.device("cuda", local_rank)
     delta = {k: s1[k] - s0[k] for k in D.AGG_FIELDS}
-    agg = D.allreduce_sum(D.group_aggregate(delta, gids % 10, 10), dist, dev)
+    nb_ = len(W.bases)
+    agg = D.allreduce_sum(D.group_aggregate(delta, gids % nb_, nb_), dist, dev)
     elapsed = D.allreduce_max(elapsed, dist, dev)
     kernel_ms = D.allreduce_max(kernel_ms, dist, dev)
     props, steps, acc = (float(agg[:, D.AGG_FIELDS.index(k)].sum()) for k in ("proposals", "steps", "accepted"))
@@ -175,40 +253,44 @@ def main():
     value = props / elapsed
     per_launch_props = props / world / args.steps
     per_launch_acc = acc / world / args.steps
-    alg_bytes = R_BYTES * per_launch_props + W_BYTES * per_launch_acc
+    alg_bytes = W.R * per_launch_props + W.W * per_launch_acc
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            if tj.get("chains") == C and tj.get("chain_steps") == args.chain_steps:
+            if (tj.get("chains") == C and tj.get("chain_steps") == args.chain_steps
+                    and tj.get("workload", "c2") == args.workload):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {
-        "metric": METRIC, "value": value, "unit": "proposals/s", "n_gpus": world, "steps": args.steps,
+        "metric": METRIC if args.workload == "c2" else f"flip proposals/sec, side workload {args.workload}",
+        "value": value, "unit": "proposals/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int8",
         "data": "synthetic: the reference's sec11 lattice and start plans, Philox stream",
-        "config": {"workload": "C2: sec11 40x40 grid (N=1596, E=3116), k=2, 4096 chains/GPU, "
-                               "base bases[g%10], alignment (g//10)%3, pop tol 0.1, seed 0x5EED0002",
-                   "graph": "sec11", "k": 2, "chains_per_gpu": C, "chain_steps_per_launch": args.chain_steps,
+        "config": {"workload": W.desc, "graph": args.workload, "k": W.k, "chains_per_gpu": C,
+                   "chain_steps_per_launch": args.chain_steps,
                    "parallelism": f"chains sharded over {world} GPU(s)"},
         "steps_per_s": steps / elapsed,
-        "per_base_proposals_per_s": {f"{b:.4g}": float(agg[i, 0]) / elapsed for i, b in enumerate(G.SEC11_BASES)},
+        "per_base_proposals_per_s": {f"{b:.4g}": float(agg[i, 0]) / elapsed for i, b in enumerate(W.bases)},
         "accept_per_proposal": acc / props if props else None,
+        "draws_per_proposal": float(agg[:, D.AGG_FIELDS.index("draws")].sum()) / props if props else None,
+        "bfs_per_proposal": float((s1["bfs_calls"] - s0["bfs_calls"]).sum()) * world / props if props else None,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "flip_k2_kernel<8>", "kernel_ms": kernel_ms,
+                     "kernel": f"flip_kernel<{fg.info['ring_max']}, 1, {2 if W.k == 2 else 0}>",
+                     "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": alg_bytes,
                      "lds": {"peak": LDS_PEAK_GBS, "frac": achieved / LDS_PEAK_GBS}},
     }
     if world == 1 and not args.no_cpu_baseline:
         cores = min(16, os.cpu_count() or 1)
         try:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cores)
-            out["cpu_baseline_c_oracle_1core"] = c_oracle_rate(min(5.0, args.cpu_seconds))
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cores, args.workload)
+            out["cpu_baseline_c_oracle_1core"] = c_oracle_rate(min(5.0, args.cpu_seconds), args.workload)
         except Exception as ex:  # report, never fake
             out["cpu_baseline"] = {"value": None, "error": repr(ex)}
     print(json.dumps(out), flush=True)

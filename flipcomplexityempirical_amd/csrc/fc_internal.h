@@ -12,6 +12,8 @@ namespace fc {
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;   // one chain per wave, 4 chains per 256-thread workgroup
+constexpr int kBigChainLds = 16 * 1024;  // above this, one chain per 64-thread workgroup (occupancy)
+inline int waves_per_block(int chain_lds_bytes) { return chain_lds_bytes > kBigChainLds ? 1 : kWavesPerBlock; }
 constexpr int kMaxK = 2;            // districts held in ChainScalars (k = 2 fast path)
 constexpr int kMaxKGeneral = 32;    // districts of the general (PAIR) kernel
 

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int c = (int)blockIdx.x * kWavesPerBlock + wv;
+    const int c = (int)blockIdx.x * (int)(blockDim.x >> 6) + wv;
     if (c >= p.n_chains) return;
 
     const int n = p.n;
@@ -307,6 +307,49 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
         }
         const bool exact = KM == 2 && (rec.meta & kMetaExact) && !force_bfs;
         const bool gam = (rec.meta & kMetaGamma) != 0;
+        // k > 2 (KM = 0): on an exact interior node (closed, fully linked ring) the flip is
+        // decided invalid when some district X != A shows up in two of the gaps between the
+        // ring's A-runs that hold old neighbours: v + an X-path closes a Jordan curve with
+        // old neighbours on both sides.  Anything else multi-run goes to the device BFS.
+        bool s_cut = false;
+        if constexpr (KM == 0) {
+            if (has && !s_lin && nA > 0 && !force_bfs && !gam && (rec.meta & kMetaExact) && (link & full) == full) {
+                uint32_t relA = 0;
+                {
+                    const uint32_t rotA = ((inA << 1) | (inA >> (Ln - 1))) & full;
+                    uint32_t st0 = inA & ~rotA;
+                    const uint32_t a2 = inA | (inA << Ln);
+                    while (st0) {
+                        const int s0 = __builtin_ctz(st0);
+                        st0 &= st0 - 1u;
+                        const int len = __builtin_ctz(~(a2 >> s0));
+                        uint32_t run = ((1u << len) - 1u) << s0;
+                        run = (run | (run >> Ln)) & full;
+                        if (run & nbr) relA |= run;
+                    }
+                }
+                const uint32_t gap = full & ~relA;
+                const uint32_t rotG = ((gap << 1) | (gap >> (Ln - 1))) & full;
+                uint32_t gst = gap & ~rotG;
+                const uint32_t g2 = gap | (gap << Ln);
+                uint32_t seen = 0;
+                while (gst && !s_cut) {
+                    const int s0 = __builtin_ctz(gst);
+                    gst &= gst - 1u;
+                    const int len = __builtin_ctz(~(g2 >> s0));
+                    uint32_t run = ((1u << len) - 1u) << s0;
+                    run = (run | (run >> Ln)) & full & ~inA;
+                    uint32_t dR = 0;
+                    while (run) {
+                        const int i = __builtin_ctz(run);
+                        run &= run - 1u;
+                        dR |= 1u << (int)a[ring_entry<RMAX>(rec.ring, i)];
+                    }
+                    s_cut = (dR & seen) != 0;
+                    seen |= dR;
+                }
+            }
+        }
         const int delta = nA - nT;  // cut(S') - cut(S)
         const bool acc = mant53(w1, w2) < T[delta + RMAX];
         // packed for the wave-uniform apply
@@ -333,6 +376,8 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
             } else if (exact) {
                 const bool touch = (av ? ng0 : ng1) > 0;  // the other district touches the outer face
                 ok = (gam && !touch) ? s_cyc : s_lin;
+            } else if (KM == 0 && s_cut) {
+                ok = false;
             } else {
                 known = s_lin;
                 ok = s_lin;
@@ -659,11 +704,18 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
 }
 
 int launch_flip_k2(const KParams &p, int ring_max, void *stream) {
-    const int blocks = (p.n_chains + kWavesPerBlock - 1) / kWavesPerBlock;
-    const size_t lds = (size_t)p.chain_lds_bytes * kWavesPerBlock;
+    const int wpb = waves_per_block(p.chain_lds_bytes);
+    const int blocks = (p.n_chains + wpb - 1) / wpb;
+    const size_t lds = (size_t)p.chain_lds_bytes * wpb;
     hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(blocks), block(kWave * kWavesPerBlock);
-#define FC_LAUNCH(R, S, K) hipLaunchKernelGGL((flip_kernel<R, S, K>), grid, block, lds, s, p)
+    const dim3 grid(blocks), block(kWave * wpb);
+#define FC_LAUNCH(R, S, K)                                                                              \
+    do {                                                                                                \
+        if (lds > 65536)                                                                                \
+            (void)hipFuncSetAttribute((const void *)flip_kernel<R, S, K>,                               \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
+        hipLaunchKernelGGL((flip_kernel<R, S, K>), grid, block, lds, s, p);                             \
+    } while (0)
 #define FC_NSUB_SWITCH(R, K)                          \
     switch (p.nsub) {                                 \
         case 1: FC_LAUNCH(R, 1, K); break;            \

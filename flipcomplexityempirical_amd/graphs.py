@@ -226,6 +226,67 @@ def strip_plan(spec: GraphSpec, k: int) -> Dict:
     return out
 
 
+def delaunay_graph(n_points: int = 10000, seed: int = 0, sigma: float = 0.5) -> GraphSpec:
+    """C5's synthetic precinct-like dual graph: the Delaunay triangulation of ``n_points``
+    uniform points in the unit square (``scipy.spatial.Delaunay``, seed 0), irregular
+    degree, node populations ``max(1, round(lognormal(0, sigma)))``."""
+    from scipy.spatial import Delaunay
+    rng = np.random.default_rng(seed)
+    pts = rng.random((n_points, 2))
+    pops = np.maximum(1, np.rint(rng.lognormal(0.0, sigma, n_points))).astype(np.int64)
+    tri = Delaunay(pts)
+    g = nx.Graph()
+    for i in range(n_points):
+        g.add_node(i, population=int(pops[i]))
+    for s in tri.simplices:
+        a, b, c = (int(x) for x in s)
+        g.add_edges_from([(a, b), (b, c), (a, c)])
+    return from_networkx(g, pos={i: (float(pts[i, 0]), float(pts[i, 1])) for i in range(n_points)})
+
+
+def bisection_plan(spec: GraphSpec, k: int) -> Dict:
+    """Recursive coordinate bisection into k districts (labels 0..k-1): split the node set
+    along its longer coordinate extent at the population quantile k1/k (k1 = k // 2),
+    recurse on both halves (C5's k=18 start plan).  Parts that come out disconnected
+    have their stray components merged into the neighbouring district they touch most."""
+    if spec.pos is None:
+        raise ValueError("bisection_plan needs node positions")
+    out = np.zeros(spec.n, dtype=np.int64)
+
+    def split(idx: np.ndarray, kk: int, first: int):
+        if kk == 1:
+            out[idx] = first
+            return
+        k1 = kk // 2
+        ext = spec.pos[idx].max(axis=0) - spec.pos[idx].min(axis=0)
+        ax = int(np.argmax(ext))
+        order = idx[np.argsort(spec.pos[idx, ax], kind="stable")]
+        cum = np.cumsum(spec.pop[order].astype(np.int64))
+        cut = int(np.searchsorted(cum, cum[-1] * k1 / kk))
+        split(order[:cut], k1, first)
+        split(order[cut:], kk - k1, first + k1)
+
+    split(np.arange(spec.n), k, 0)
+    # repair: keep the largest component of each district, hand the rest to a neighbour
+    g = spec.nx_graph
+    for _ in range(4):
+        changed = False
+        for d in range(k):
+            nodes = [spec.nodes[i] for i in np.nonzero(out == d)[0]]
+            comps = sorted(nx.connected_components(g.subgraph(nodes)), key=len, reverse=True)
+            for comp in comps[1:]:
+                for nd in comp:
+                    i = spec.index[nd]
+                    votes = np.bincount([out[spec.index[w]] for w in g.neighbors(nd) if out[spec.index[w]] != d],
+                                        minlength=k)
+                    if votes.sum():
+                        out[i] = int(np.argmax(votes))
+                        changed = True
+        if not changed:
+            break
+    return {spec.nodes[i]: int(out[i]) for i in range(spec.n)}
+
+
 # --------------------------------------------------------------------------------------
 # Known answers used by tests (host-side, networkx)
 # --------------------------------------------------------------------------------------

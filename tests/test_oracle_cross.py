@@ -102,3 +102,35 @@ def test_pair_k2_equals_bi_sign(cref, sec11):
     r1 = cref.run(sec11, a0, proposal=1, **kw)
     assert np.array_equal(r0["trace"], r1["trace"])
     assert r0["stats"] == r1["stats"]
+
+
+def test_c_oracle_pair_delaunay_equals_gc_faithful(cref):
+    """Irregular planar dual graph with non-unit populations (C5's family), k = 6."""
+    from oracle.flipref import GcFaithfulChain
+    spec = G.delaunay_graph(300, seed=3)
+    k = 6
+    plan = G.bisection_plan(spec, k)
+    a0 = spec.assignment_array(plan, list(range(k)))
+    l1 = G.log1mp_table(spec.n, k)
+    (lo, hi), (ilo, ihi) = G.population_bounds(int(spec.pop.sum()), k, 0.1)
+    gc = GcFaithfulChain(spec, plan, base=1.5, pop_bounds=(lo, hi), seed=8, chain_id=1, log1mp=l1,
+                         pair=True).run(300)
+    r = cref.run(spec, a0, base=1.5, pop_lo=ilo, pop_hi=ihi, seed=8, chain_id=1, n_steps=300, k=k,
+                 labels=list(range(k)), log1mp=l1, trace_cap=100000, proposal=1)
+    gtr = np.array(gc.trace, dtype=np.int64)
+    assert len(r["trace"]) == len(gtr)
+    for i, f in enumerate(["draw", "v", "flags", "cut", "nb", "wait"]):
+        assert np.array_equal(r["trace"][f], gtr[:, i]), f
+    assert np.array_equal(gc.assignment_ids(), r["final"])
+
+
+def test_bisection_plan_is_valid():
+    import networkx as nx
+    spec = G.delaunay_graph(2000, seed=1)
+    plan = G.bisection_plan(spec, 18)
+    a = spec.assignment_array(plan, list(range(18)))
+    _, _, pops = G.cut_and_boundary(spec, a)
+    (lo, hi), _ = G.population_bounds(int(spec.pop.sum()), 18, 0.1)
+    assert pops.min() >= lo and pops.max() <= hi
+    for d in range(18):
+        assert nx.is_connected(spec.nx_graph.subgraph([n for n in spec.nodes if plan[n] == d]))

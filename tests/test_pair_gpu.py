@@ -110,3 +110,16 @@ def test_pair_rejects_bad_config(gpu, sec11):
     with pytest.raises(NotImplementedError):
         FlipRun(fg, a0, RunConfig(k=40, labels=tuple(range(40)), proposal=_lib.FC_PROPOSE_PAIR,
                                   pop_lo=0, pop_hi=10 ** 6))
+
+
+@pytest.mark.parametrize("n_points,steps", [(2000, 3000), (10000, 1500)])
+def test_c5_delaunay_k18_pair_parity(gpu, cref, n_points, steps):
+    """C5: Delaunay dual of uniform points (irregular degree up to 16), lognormal
+    populations, k = 18 recursive-bisection plan, pop tolerance 0.1."""
+    spec = G.delaunay_graph(n_points, seed=0)
+    k = 18
+    a0 = spec.assignment_array(G.bisection_plan(spec, k), list(range(k)))
+    inits = np.stack([a0] * 8)
+    bases = np.asarray([0.5, 1.0, 2.0, 4.0] * 2)
+    run = _run_pair(spec, inits, bases, k, steps=steps, pct=0.1)
+    _check(cref, spec, run, k, inits, bases, steps=steps, pct=0.1)
