@@ -11,9 +11,13 @@ import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
-LIB = os.path.join(PKG, "libflipchain.so")
-SOURCES = ["fc_kernels.hip", "fc_series.hip", "fc_capi.cpp", "fc_graph.cpp"]
-HEADERS = ["fc_internal.h", "fc_philox.h", os.path.join("..", "..", "include", "flipchain.h")]
+# FC_LIB_VARIANT selects a diagnostic build: "_"-separated tokens, each a -D flag
+# (prof: per-phase s_memtime counters).
+VARIANT = os.environ.get("FC_LIB_VARIANT", "")
+VARIANT_FLAGS = {"prof": "-DFC_PHASE_PROF"}
+LIB = os.path.join(PKG, f"libflipchain_{VARIANT}.so" if VARIANT else "libflipchain.so")
+SOURCES = ["fc_flip2.hip", "fc_kernels.hip", "fc_series.hip", "fc_capi.cpp", "fc_graph.cpp"]
+HEADERS = ["fc_internal.h", "fc_philox.h", "fc_device.h", os.path.join("..", "..", "include", "flipchain.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("FC_OFFLOAD_ARCH", "gfx950")
 
@@ -31,6 +35,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-o", LIB]
+    for tok in filter(None, VARIANT.split("_")):
+        cmd.insert(-2, VARIANT_FLAGS[tok])
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), flush=True)

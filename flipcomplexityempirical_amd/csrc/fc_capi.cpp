@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -51,6 +52,7 @@ struct fc_run {
     fc_record *d_trace = nullptr;
     uint32_t *d_tape = nullptr;
     int64_t tape_draws = 0;
+    int64_t *d_prof = nullptr;  // FC_PHASE_PROF builds
 };
 
 namespace {
@@ -81,7 +83,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc, r->d_edge_since,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events, r->d_prof};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -234,7 +236,10 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     r->n_chains = n_chains;
     r->npad = (n + 15) & ~15;
     r->words = (n + 63) / 64;
-    r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + 3 * r->words * 8 + 5 * 64 * 4 + fc::kMaxKGeneral * 4;
+    if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, BFS bitmaps, slots, commit marks (2 npad + 16)
+        r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 3 * r->words * 8 + 4 * 64 * 4 + 16;
+    else         // fc_kernels.hip: a, fcnt, thresholds, BFS bitmaps, slots, district populations
+        r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + 3 * r->words * 8 + 5 * 64 * 4 + fc::kMaxKGeneral * 4;
     r->wmax = 1;
     if (k > 2) r->wmax = p->wmax > 0 ? p->wmax : std::max(1, std::min(g.max_degree, k - 1));
     r->chain_lds_bytes = (r->chain_lds_bytes + 15) & ~15;
@@ -456,11 +461,21 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.ev_cap = r->ev_cap;
     k.hit_lo = r->p.hit_lo;
     k.hit_hi = r->p.hit_hi;
-    k.nsub = 1;
+    k.nsub = r->p.k == 2 ? 2 : 1;  // k = 2: up to two rounds of 64 draws per batch
     if (const char *e = std::getenv("FC_NSUB")) k.nsub = std::atoi(e);
     k.hit_stop = 32;
     if (const char *e = std::getenv("FC_HIT_STOP")) k.hit_stop = std::atoi(e);
+    k.par_min = 3;
+    if (const char *e = std::getenv("FC_PAR_MIN")) k.par_min = std::atoi(e);
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : r->stream;
+    k.prof = nullptr;
+#ifdef FC_PHASE_PROF
+    if (!r->d_prof) {
+        if (int rc = dalloc(&r->d_prof, (size_t)r->n_chains * fc::kProfSlots)) return rc;
+    }
+    HIP_TRY(hipMemsetAsync(r->d_prof, 0, (size_t)r->n_chains * fc::kProfSlots * 8, s));
+    k.prof = r->d_prof;
+#endif
     if (r->n_launch_events == r->launch_events.size()) {
         hipEvent_t a, b;
         HIP_TRY(hipEventCreate(&a));
@@ -474,10 +489,21 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     for (int64_t done = 0; done < n_steps; done += kChunk) {
         k.n_steps = std::min(kChunk, n_steps - done);
         if (max_draws <= 0) k.max_draws = 65536 * k.n_steps;
-        const int e = fc::launch_flip_k2(k, r->g.ring_max, s);
+        const int e = r->p.k == 2 ? fc::launch_flip2(k, r->g.ring_max, s) : fc::launch_flip_k2(k, r->g.ring_max, s);
         if (e != 0) return fail(FC_ERR_HIP, std::string("flip kernel launch: ") + hipGetErrorString((hipError_t)e));
     }
     HIP_TRY(hipEventRecord(evp.second, s));
+#ifdef FC_PHASE_PROF
+    if (const char *path = std::getenv("FC_PROF_OUT")) {
+        std::vector<int64_t> h((size_t)r->n_chains * fc::kProfSlots);
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipMemcpy(h.data(), r->d_prof, h.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE *f = std::fopen(path, "ab")) {
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+        }
+    }
+#endif
     r->ev0 = evp.first;
     r->ev1 = evp.second;
     ++r->n_launch_events;

@@ -1,0 +1,752 @@
+// Two-district flip-walk kernel for gfx950 (MI355X): the headline path.
+//
+// Reference step: MarkovChain.__next__ [gc-0.2] driving slow_reversible_propose_bi,
+// single_flip_contiguous + within_percent_of_ideal_population and cut_accept
+// (grid_chain_sec11.py:132-179, 299-342), plus the driver's per-yield diagnostics
+// (:366-402).  k = 2 is the reference's only configuration; PAIR proposals with k = 2
+// coincide with it (one foreign district).
+//
+// One chain per wavefront, state in LDS (int8 district, uint8 foreign-neighbour count per
+// node; |B| and boundary membership are O(1)).  A wave advances its chain in batches:
+//   1. up to NSUB rounds of 64 Philox draws map to nodes (exact Lemire); draws on boundary
+//      nodes are proposals (rejection sampling of random.choice over b_nodes,
+//      grid_chain_sec11.py:143) and are packed, in draw order, into up to 64 slots; the
+//      nodes of the other ("non-hit") draws stay in registers;
+//   2. every slot is evaluated against the current state: ring districts, contiguity by the
+//      planar run rule, population bound, delta-cut, Metropolis threshold;
+//   3. commit in draw order.  One event at a time when few slots of the batch accept: the
+//      first acceptance is applied and every later slot whose view it changed (the flipped
+//      node in its ring or as its node) ends the batch, as does the first later non-hit
+//      draw whose node it pulled into the boundary.  When many accept, a segment-parallel
+//      commit (commit marks in LDS + prefix scans, below) applies them in one pass.  Either
+//      way the committed sequence is the one-draw-at-a-time chain, bit for bit;
+//   4. the per-yield diagnostics are accumulated lane-parallel from per-slot status bits.
+#include <hip/hip_runtime.h>
+
+#include "fc_device.h"
+#include "fc_internal.h"
+#include "fc_philox.h"
+
+namespace fc {
+
+using namespace dev;
+
+template <int RMAX, int NSUB, bool FULL>
+__global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = (int)(threadIdx.x & 63u);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int c = (int)blockIdx.x * (int)(blockDim.x >> 6) + wv;
+    if (c >= p.n_chains) return;
+
+    const int n = p.n;
+    const int npad = (n + 15) & ~15;
+    unsigned char *base = smem + (size_t)wv * p.chain_lds_bytes;
+    int8_t *a = (int8_t *)base;                    // [npad] district of each node
+    uint8_t *fcnt = base + npad;                   // [npad] foreign neighbours of each node
+    uint64_t *T = (uint64_t *)(base + 2 * npad);   // [2 RMAX + 2] acceptance thresholds by delta-cut
+    uint64_t *vis = T + (2 * RMAX + 2);            // BFS bitmaps [words] x 3
+    uint64_t *front = vis + p.words;
+    uint64_t *nxt = front + p.words;
+    uint32_t *slot = (uint32_t *)(nxt + p.words);  // [4][64]: node, word1, word2, draw offset
+    uint8_t *smark = (uint8_t *)(slot + 4 * 64);   // [npad] lowest slot of a segment flip at the node
+    uint8_t *nmark = smark + npad;                 // [npad] ... having the node as a neighbour
+    uint8_t *const dum = nmark + npad + (lane & 15);  // [16] sink for masked-off stores
+    const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
+
+    // ---- load the chain into LDS -------------------------------------------------------
+    {
+        const uint4 *ga = (const uint4 *)(p.assign + (size_t)c * npad);
+        const uint4 *gf = (const uint4 *)(p.fcnt + (size_t)c * npad);
+        for (int i = lane; i < npad / 16; i += kWave) {
+            ((uint4 *)a)[i] = ga[i];
+            ((uint4 *)fcnt)[i] = gf[i];
+        }
+        if (lane < 2 * RMAX + 1) T[lane] = p.thresh[(size_t)c * (2 * RMAX + 1) + lane];
+        for (int i = lane; i < npad / 4 + 2; i += kWave) ((uint64_t *)smark)[i] = ~0ull;  // marks + sink
+    }
+    ChainScalars *scp = p.sc + c;
+    uint64_t draw = scp->draw;
+    int64_t steps = scp->steps;  // index of the current yield
+    int64_t bfs_calls = scp->bfs_calls, bfs_levels = scp->bfs_levels;
+    int64_t trace_len = FULL ? scp->trace_len : 0;
+    int64_t ev_len = FULL ? scp->ev_len : 0, hit_time = FULL ? scp->hit_time : 0;
+    int cut = scp->cut, nb = scp->nb;
+    int pops0 = scp->pops[0], pops1 = scp->pops[1];
+    int ng0 = scp->ngamma[0], ng1 = scp->ngamma[1];
+    int64_t wait_cur = scp->wait_cur;
+    int last_flip = scp->last_flip;
+    int stuck = 0;
+    int rem = (int)p.n_steps;  // steps still to take in this launch (host: n_steps < 2^31)
+    uint64_t draw_cap = draw + (uint64_t)p.max_draws;
+    if (FULL && p.tape && draw_cap > (uint64_t)p.tape_draws) draw_cap = (uint64_t)p.tape_draws;
+    const uint32_t chain_gid = p.chain_id_offset + (uint32_t)c;
+    const bool force_bfs = (p.flags & FC_FLAG_FORCE_BFS) != 0;
+    const bool want_wait = (p.diag & FC_DIAG_WAIT) != 0;
+    const bool trace_on = FULL && p.trace && c < p.trace_chains;
+
+    // per-lane accumulators, reduced once per launch
+    int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
+    uint32_t n_prop = 0, n_acc = 0, n_ic = 0, n_ip = 0;
+#ifdef FC_PHASE_PROF
+    int64_t prof_acc[kProfSlots] = {};
+#endif
+    wave_sync();
+    FC_STAMP(t_loop0);
+
+    while (rem > 0) {
+        FC_STAMP(t_a);
+        FC_PROF(5, 1);
+        if (draw >= draw_cap) {
+            stuck = 1;
+            break;
+        }
+        const uint64_t room = draw_cap - draw;
+        // ---- 1. draws -> nodes; boundary hits packed, in draw order, into <= 64 slots ----
+        int nh = 0;   // boundary hits seen
+        int gen = 0;  // draws generated (offsets 0..gen-1 of this batch)
+        int rv[NSUB]; // node of this lane's non-hit draw in round r (offset 64 r + lane), -1: none
+#pragma unroll
+        for (int r = 0; r < NSUB; ++r) {
+            rv[r] = -1;
+            if ((r > 0 && nh >= p.hit_stop) || nh >= 64 || (uint64_t)gen >= room) continue;
+            const int off = gen + lane;
+            const bool inrange = (uint64_t)off < room;
+            const uint64_t dr = draw + (uint64_t)off;
+            Words4 w;
+            if (FULL && p.tape) {
+                const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + (inrange ? dr : draw)) * 6;
+                w = Words4{t[0], t[1], t[2], t[3]};
+            } else {
+                w = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
+            }
+            const uint64_t m = (uint64_t)w.x0 * (uint64_t)(uint32_t)n;
+            const int vd = (int)(m >> 32);
+            const bool okd = inrange && (uint32_t)m >= p.lemire_thresh;
+            const bool hitd = okd && fcnt[vd] != 0;
+            const uint64_t hm = __ballot(hitd);
+            const int sp = nh + count_below(hm);
+            if (hitd && sp < 64) {
+                slot[sp] = (uint32_t)vd;
+                slot[64 + sp] = w.x1;
+                slot[128 + sp] = w.x2;
+                slot[192 + sp] = (uint32_t)off;
+            }
+            const int cnt = __popcll(hm);
+            int used = kWave;  // lanes of this round consumed by the batch
+            if (nh + cnt > 64) {  // the 64th hit closes the batch inside this round
+                used = kth_set_bit(hm, 64 - nh) + 1;
+                gen += used;
+            } else {
+                gen = (uint64_t)(gen + 64) < room ? gen + 64 : (int)room;
+            }
+            if (okd && !hitd && lane < used) rv[r] = vd;
+            nh += cnt;
+        }
+        const int ns = nh < 64 ? nh : 64;
+        compiler_fence();
+        FC_STAMP(t_b);
+        FC_PROF(1, t_b - t_a);
+
+        // ---- 2. every slot against the current state --------------------------------------
+        const bool has = lane < ns;
+        const int off_l = has ? (int)slot[192 + lane] : gen;
+        const uint64_t d = draw + (uint64_t)off_l;
+        const int v = has ? (int)slot[lane] : 0;
+        const uint32_t w1 = slot[64 + lane], w2 = slot[128 + lane];
+        const NodeRec<RMAX> rec = G[v];
+        const int av = a[v];
+        const int pv = rec.pop;
+        const uint32_t Ln = (uint32_t)(rec.meta & kMetaLenMask);
+        const uint32_t full = (1u << Ln) - 1u;
+        const uint32_t nbr = (uint32_t)(rec.meta >> kMetaNbrShift) & 0xffffu;
+        const uint32_t link = (uint32_t)(rec.meta >> kMetaLinkShift) & 0xffffu;
+        int cell[RMAX];  // ring cells (padded with the node itself)
+        uint32_t inA = 0;
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) {
+            cell[i] = ring_entry<RMAX>(rec.ring, i);
+            inA |= (uint32_t)(a[cell[i]] == av) << i;
+        }
+        inA &= full;
+        const int tgt = 1 - av;                 // -1 * assignment, grid_chain_sec11.py:145
+        const uint32_t nbrA = inA & nbr;        // old-district neighbours
+        const uint32_t tmask = nbr & ~inA;      // target-district neighbours
+        const int nA = __popc(nbrA);
+        const int delta = nA - __popc(tmask);   // cut(S') - cut(S)
+        const bool hit = has && tmask != 0u;    // v in b_nodes: a proposal
+        bool s_lin, s_cyc;
+        {
+            const uint32_t rot = Ln ? (((inA >> 1) | (inA << (Ln - 1))) & full) : 0u;
+            const uint32_t lk = inA & rot & link;
+            s_lin = one_run(nbrA, full & ~lk, full);
+            const uint32_t vlink = (Ln >= 2 && (inA & 1u) && ((inA >> (Ln - 1)) & 1u)) ? (1u << (Ln - 1)) : 0u;
+            s_cyc = one_run(nbrA, full & ~(lk | vlink), full);
+        }
+        const bool exact = (rec.meta & kMetaExact) && !force_bfs;
+        const bool gam = (rec.meta & kMetaGamma) != 0;
+        const bool acc = mant53(w1, w2) < T[delta + RMAX];
+        FC_STAMP(t_c);
+        FC_PROF(2, t_c - t_b);
+
+        // ---- 3. commit in draw order ----------------------------------------------------
+        uint32_t st = 0;
+        int end = ns, pos = 0;
+        int trunc_off = gen;  // first draw offset not consumed by this batch
+        bool target_hit = false;
+        const int cut0 = cut, nb0 = nb, rem0 = rem;
+        const int64_t steps0 = steps;
+        const int last_flip0 = last_flip;
+        const int a_last0 = FULL && last_flip0 >= 0 ? (int)a[last_flip0] : 0;
+        int cut_after = 0, nb_after = 0;
+        const int dp_l = av == 0 ? -pv : pv;            // pops0 change of this lane's flip
+        const int dg_l = gam ? (av == 0 ? -1 : 1) : 0;  // ngamma0 change
+        bool wrote = false;                              // this lane holds commit marks
+
+        // contiguity undecided by the ring rule at lane f: wave BFS on the current state
+        auto run_bfs = [&](int f) -> bool {
+            const uint32_t nbrAf = rlu(nbrA, f);
+            int my_target = -1, start = -1;
+#pragma unroll
+            for (int k2 = 0; k2 < RMAX / 2; ++k2) {
+                const uint32_t wrd = rlu(rec.ring[k2], f);
+                if ((lane >> 1) == k2) my_target = (int)((wrd >> (16 * (lane & 1))) & 0xffffu);
+                if (start < 0 && ((nbrAf >> (2 * k2)) & 1u)) start = (int)(wrd & 0xffffu);
+                if (start < 0 && ((nbrAf >> (2 * k2 + 1)) & 1u)) start = (int)(wrd >> 16);
+            }
+            if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
+            ++bfs_calls;
+            return wave_bfs<RMAX>(G, a, vis, front, nxt, p.words, lane, rl32(v, f), rl32(av, f), my_target, start,
+                                  bfs_levels);
+        };
+
+        while (pos < end) {
+            FC_PROF(6, 1);
+            const bool prop = hit && lane >= pos && lane < end;
+            // contiguity verdict when the other district does (okT) / does not (okN) touch
+            // the outer face -- the outer-face counts are chain-global
+            bool known = true, okT, okN;
+            if (st & ST_BD) {
+                okT = okN = (st & ST_BR) != 0;
+            } else if (nA == 0) {
+                okT = okN = false;
+            } else if (exact) {
+                okT = s_lin;
+                okN = gam ? s_cyc : s_lin;
+            } else {
+                known = s_lin;
+                okT = okN = s_lin;
+            }
+            const bool ok = ((av ? ng0 : ng1) > 0) ? okT : okN;
+            const int pa = av ? pops1 : pops0, pb = av ? pops0 : pops1;
+            const bool popok = (pa - pv >= p.pop_lo) && (pb + pv <= p.pop_hi);
+            const bool valid = prop && known && ok && popok;
+            const uint64_t C0 = __ballot(valid && acc);
+            if (__popcll(C0) >= p.par_min) {
+                FC_PROF(12, 1);
+                // ---- segment-parallel commit ---------------------------------------------
+                // A lane's verdict reads only a[] on its node and ring, so it stays exact until
+                // a flip lands there (alpha: the batch ends at that lane; a non-hit lane ends
+                // it when a flip lands on a neighbour, its node entering the boundary); two
+                // flips sharing a neighbour would need ordered foreign-count updates (beta: the
+                // batch ends at the later one).  Inside a segment the flips then commute except
+                // through the chain-global populations and outer-face counts: a prefix scan over
+                // the speculative acceptances gives every lane its sequential view, and the
+                // first lane whose verdict changes under that view closes the segment (it is
+                // itself exact).  Flips committed one at a time (below) leave no marks: they cut
+                // the batch at every lane they affect themselves.
+                const bool cand0 = valid && acc;
+                const int x0 = cand0 ? dp_l : 0;
+                const int P = wave_scan_incl(x0) - x0;
+                const int Gp = count_below(__ballot(cand0 && dg_l > 0)) - count_below(__ballot(cand0 && dg_l < 0));
+                const bool ok1 = ((av ? ng0 + Gp : ng1 - Gp) > 0) ? okT : okN;
+                const int q0 = pops0 + P, q1 = pops1 - P;
+                const bool valid1 = prop && known && ok1 && ((av ? q1 : q0) - pv >= p.pop_lo) &&
+                                    ((av ? q0 : q1) + pv <= p.pop_hi);
+                const bool cand1 = valid1 && acc;
+                const uint64_t MM = __ballot(prop && cand1 != cand0);
+                const uint64_t UU = __ballot(prop && !known);
+                int sg = end;
+                if (MM) sg = min(sg, __builtin_ctzll(MM) + 1);
+                const int u = UU ? __builtin_ctzll(UU) : kWave;
+                if (u < sg) sg = u;
+                uint64_t VAL = __ballot(valid1) & lane_range(pos, sg);
+                bool last_step = false;
+                if (__popcll(VAL) >= rem) {  // the launch's last step lies in this segment
+                    sg = kth_set_bit(VAL, rem) + 1;
+                    VAL &= bits_below(sg);
+                    last_step = true;
+                }
+                const uint64_t K = __ballot(cand1) & lane_range(pos, sg);
+                int x = kWave;  // first lane that must not be committed
+                if (K) {
+                    const bool inK = (K >> lane) & 1ull;
+                    wrote |= inK;
+                    // marks: smark[node] / nmark[neighbour] = lowest candidate lane (0xff: none)
+                    bool need = inK;
+                    int ms, mn[RMAX];
+                    for (;;) {
+                        ms = smark[v];
+#pragma unroll
+                        for (int i = 0; i < RMAX; ++i) mn[i] = nmark[cell[i]];
+                        compiler_fence();
+                        *((need && ms > lane) ? &smark[v] : dum) = (uint8_t)lane;
+#pragma unroll
+                        for (int i = 0; i < RMAX; ++i)
+                            *((need && ((nbr >> i) & 1u) && mn[i] > lane) ? &nmark[cell[i]] : dum) = (uint8_t)lane;
+                        compiler_fence();
+                        ms = smark[v];
+                        bool again = ms > lane;
+#pragma unroll
+                        for (int i = 0; i < RMAX; ++i) {
+                            mn[i] = nmark[cell[i]];
+                            again |= ((nbr >> i) & 1u) && mn[i] > lane;
+                        }
+                        need = need && again;
+                        if (!__any(need)) break;
+                    }
+                    // alpha (later proposals), entering non-hits and beta (later candidates)
+                    bool conf = hit && ms < lane;
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i) {
+                        const bool nb_i = (nbr >> i) & 1u;
+                        conf |= hit && (int)smark[cell[i]] < lane;
+                        conf |= inK && nb_i && mn[i] < lane;
+                    }
+                    const uint64_t XX = __ballot(conf && lane > pos && lane < end);
+                    if (XX) x = __builtin_ctzll(XX);
+                    // non-hit draws whose node a committed flip pulls into the boundary would
+                    // now be proposals: the batch ends before the first of them
+                    int t = trunc_off;
+#pragma unroll
+                    for (int r = 0; r < NSUB; ++r) {
+                        const int mk = nmark[rv[r] < 0 ? 0 : rv[r]];
+                        const bool tr = rv[r] >= 0 && mk < x && 64 * r + lane > (int)slot[192 + (mk & 63)];
+                        const uint64_t TR = __ballot(tr);
+                        if (TR) t = min(t, 64 * r + __builtin_ctzll(TR));
+                    }
+                    if (t < trunc_off) {
+                        trunc_off = t;
+                        const int e2 = __popcll(__ballot(has && off_l < t));
+                        if (e2 < x) x = e2;
+                    }
+                }
+                const int ce = min(sg, x);  // commit lanes [pos, ce)
+                if (x < sg) last_step = false;
+                if (x < end) end = x;
+                if (prop && lane < ce) st |= valid1 ? (cand1 ? (ST_VS | ST_AC) : ST_VS) : (ok1 ? ST_IP : ST_IC);
+                rem -= __popcll(VAL & bits_below(ce));
+                const uint64_t AP = K & bits_below(ce);
+                if (AP) {
+                    FC_PROF(7, __popcll(AP));
+                    const bool me = (AP >> lane) & 1ull;
+                    // foreign-neighbour counts: u sees v leave A (+1 if u in A) and join t (-1 if u
+                    // in t); beta leaves every u to one flip of the segment
+                    int oldc[RMAX];
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i) oldc[i] = fcnt[cell[i]];
+                    compiler_fence();
+                    int dnb = 0;
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i) {
+                        const bool nb_i = me && ((nbr >> i) & 1u);
+                        const int dlt = (int)((inA >> i) & 1u) - (int)((tmask >> i) & 1u);
+                        *(nb_i ? &fcnt[cell[i]] : dum) = (uint8_t)(oldc[i] + dlt);
+                        dnb += nb_i ? (int)(dlt > 0 && oldc[i] == 0) - (int)(dlt < 0 && oldc[i] == 1) : 0;
+                    }
+                    *(me ? (uint8_t *)&a[v] : dum) = (uint8_t)tgt;
+                    *(me ? &fcnt[v] : dum) = (uint8_t)nA;
+                    const int pkd = me ? ((delta + 32) | ((dnb + 32) << 16)) : 0;
+                    const int S = wave_scan_incl(pkd);
+                    const int cntA = count_below(AP) + 1;
+                    if (me) {
+                        cut_after = cut + (S & 0xffff) - 32 * cntA;
+                        nb_after = nb + (S >> 16) - 32 * cntA;
+                    }
+                    const int L = 63 - __builtin_clzll(AP);
+                    cut = rl32(cut_after, L);
+                    nb = rl32(nb_after, L);
+                    const int dP = rl32(P + dp_l, L), dG = rl32(Gp + dg_l, L);
+                    pops0 += dP;
+                    pops1 -= dP;
+                    ng0 += dG;
+                    ng1 -= dG;
+                    last_flip = rl32(v, L);
+                    compiler_fence();
+                }
+                pos = ce;
+                if (last_step) {
+                    end = pos;
+                    target_hit = true;
+                    break;
+                }
+                if (pos >= end) break;
+                if (u == pos) {
+                    const bool res = run_bfs(u);
+                    if (lane == u) st |= ST_BD | (res ? ST_BR : 0u);
+                }
+                continue;
+            }
+            // ---- one event at a time: the first acceptance or undecided lane -----------------
+            const uint64_t VAL = __ballot(valid);
+            const uint64_t EV = C0 | __ballot(prop && !known);
+            const int f = EV ? __builtin_ctzll(EV) : end;
+            const uint64_t segv = VAL & bits_below(f);
+            const int nvalid = __popcll(segv);
+            const uint32_t bits = valid ? ST_VS : (ok ? ST_IP : ST_IC);
+            if (nvalid >= rem) {  // the launch's last step lies before f
+                const int e = kth_set_bit(segv, rem);
+                if (prop && lane <= e) st |= bits;
+                rem = 0;
+                end = e + 1;
+                target_hit = true;
+                break;
+            }
+            if (prop && lane < f) st |= bits;
+            rem -= nvalid;
+            pos = f;
+            if (f >= end) break;
+            if (!((VAL >> f) & 1ull)) {
+                const bool res = run_bfs(f);
+                if (lane == f) st |= ST_BD | (res ? ST_BR : 0u);
+                continue;
+            }
+            // ---- accept lane f: apply the flip -------------------------------------------------
+            FC_PROF(7, 1);
+            const int vf = rl32(v, f), Af = rl32(av, f), pvf = rl32(pv, f), df = rl32(delta, f);
+            const uint32_t inAf = rlu(inA, f), nbrf = rlu(nbr, f), tmf = rlu(tmask, f);
+            const bool gamf = rl32((int)gam, f) != 0;
+            uint32_t rw[RMAX / 2];
+#pragma unroll
+            for (int k2 = 0; k2 < RMAX / 2; ++k2) rw[k2] = rlu(rec.ring[k2], f);
+            uint32_t sel = rw[0];
+#pragma unroll
+            for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((lane >> 1) == k2) ? rw[k2] : sel;
+            const int my_e = (int)((sel >> (16 * (lane & 1))) & 0xffffu);
+            const bool is_nbr = lane < RMAX && ((nbrf >> lane) & 1u);
+            // foreign-neighbour counts: u sees v leave A (+1 if u in A) and join t (-1 if u in t)
+            const int dlt = (int)((inAf >> lane) & 1u) - (int)((tmf >> lane) & 1u);
+            bool enter = false, leave = false;
+            if (is_nbr) {
+                const int old = fcnt[my_e];
+                fcnt[my_e] = (uint8_t)(old + dlt);
+                enter = dlt > 0 && old == 0;
+                leave = dlt < 0 && old == 1;
+            }
+            if (lane == 0) {
+                a[vf] = (int8_t)(1 - Af);
+                fcnt[vf] = (uint8_t)__popc(nbrf & inAf);
+            }
+            // later lanes whose view the flip changed: proposals with vf in their ring or as
+            // their node (rings are symmetric), non-hits with vf as a neighbour
+            uint32_t eqm = 0;
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) eqm |= (uint32_t)(cell[i] == vf) << i;
+            const bool stale = hit && (v == vf || eqm != 0u);
+            const uint64_t aff = __ballot(stale && lane > f && lane < end);
+            if (aff) end = __builtin_ctzll(aff);
+            uint64_t ent = __ballot(enter);
+            const int dnb = __popcll(ent) - __popcll(__ballot(leave));
+            // non-hit draws after f whose node just entered the boundary would now propose
+            if (ent) {
+                const int off_f = rl32(off_l, f);
+                int t_na = trunc_off;
+                while (ent) {
+                    const int un = rl32(my_e, __builtin_ctzll(ent));
+                    ent &= ent - 1;
+#pragma unroll
+                    for (int r = 0; r < NSUB; ++r) {
+                        const uint64_t m2 = __ballot(rv[r] == un && 64 * r + lane > off_f);
+                        if (m2) t_na = min(t_na, 64 * r + __builtin_ctzll(m2));
+                    }
+                }
+                if (t_na < trunc_off) {
+                    trunc_off = t_na;
+                    const int e2 = __popcll(__ballot(has && off_l < t_na));
+                    if (e2 < end) end = e2;
+                }
+            }
+            if (Af == 0) {
+                pops0 -= pvf;
+                pops1 += pvf;
+            } else {
+                pops1 -= pvf;
+                pops0 += pvf;
+            }
+            if (gamf) {
+                const int dg = Af == 0 ? -1 : 1;
+                ng0 += dg;
+                ng1 -= dg;
+            }
+            cut += df;
+            nb += dnb;
+            --rem;
+            last_flip = vf;
+            if (lane == f) {
+                st |= ST_VS | ST_AC;
+                cut_after = cut;
+                nb_after = nb;
+            }
+            compiler_fence();
+            pos = f + 1;
+            if (rem == 0) {
+                end = pos;
+                target_hit = true;
+                break;
+            }
+        }
+        if (wrote) {  // clear this lane's marks for the next batch
+            smark[v] = 0xff;
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) *(((nbr >> i) & 1u) ? &nmark[cell[i]] : dum) = 0xff;
+        }
+        compiler_fence();
+        steps = steps0 + (rem0 - rem);
+        FC_STAMP(t_d);
+        FC_PROF(3, t_d - t_c);
+
+        // ---- 4. lane-parallel bookkeeping of the committed draws [0, end) ------------------
+        const bool done = lane < end;
+        const bool is_acc = (st & ST_AC) != 0;
+        n_prop += (hit && done) ? 1u : 0u;
+        n_acc += is_acc ? 1u : 0u;
+        n_ic += (st & ST_IC) ? 1u : 0u;
+        n_ip += (st & ST_IP) ? 1u : 0u;
+        const uint64_t ACCM = __ballot(is_acc);
+        const uint64_t VSM = __ballot((st & ST_VS) != 0);
+        const uint64_t later_acc = ACCM & ~bits_below(lane + 1);
+        const int next_acc = later_acc ? __builtin_ctzll(later_acc) : end;
+        const int run_len = is_acc ? 1 + __popcll(VSM & lane_range(lane + 1, next_acc)) : 0;
+        const int first_acc = ACCM ? __builtin_ctzll(ACCM) : end;
+        const int r0 = __popcll(VSM & bits_below(first_acc));
+        int64_t my_wait = 0;
+        if (want_wait && is_acc) {
+            Words4 g;
+            if (FULL && p.tape) {
+                const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + d) * 6;
+                g = Words4{t[4], t[5], 0u, 0u};
+            } else {
+                g = philox4x32_10((uint32_t)d, (uint32_t)(d >> 32), chain_gid, 1u, p.seed_lo, p.seed_hi);
+            }
+            my_wait = geom_from(u53(g.x0, g.x1), p.log1mp[nb_after]);
+        }
+        if (is_acc) {
+            acc_cut += (int64_t)cut_after * run_len;
+            acc_cut2 += (int64_t)cut_after * cut_after * run_len;
+            acc_nb += (int64_t)nb_after * run_len;
+            acc_nb2 += (int64_t)nb_after * nb_after * run_len;
+            acc_wait += my_wait * run_len;
+        }
+        if (lane == 0 && r0) {
+            acc_cut += (int64_t)cut0 * r0;
+            acc_cut2 += (int64_t)cut0 * cut0 * r0;
+            acc_nb += (int64_t)nb0 * r0;
+            acc_nb2 += (int64_t)nb0 * nb0 * r0;
+            acc_wait += wait_cur * r0;
+        }
+        if constexpr (FULL) {
+            const int64_t t_acc = steps0 + __popcll(VSM & bits_below(lane + 1));  // yield index of this lane
+            if ((p.diag & FC_DIAG_SERIES) && ACCM) {
+                const int64_t idx = ev_len + __popcll(ACCM & bits_below(lane));
+                if (is_acc && idx < p.ev_cap) {
+                    fc_event ev;
+                    ev.t = t_acc;
+                    ev.v = (uint16_t)v;
+                    ev.cut = (uint16_t)cut_after;
+                    ev.nb = (uint16_t)nb_after;
+                    ev.target = (uint8_t)tgt;
+                    ev.reserved = 0;
+                    p.events[(size_t)c * p.ev_cap + idx] = ev;
+                }
+                ev_len += __popcll(ACCM);
+            }
+            if (hit_time < 0 && ACCM) {
+                const uint64_t hm = __ballot(is_acc && cut_after >= p.hit_lo && cut_after <= p.hit_hi);
+                if (hm) {
+                    const int hl = __builtin_ctzll(hm);
+                    hit_time = steps0 + __popcll(VSM & bits_below(hl + 1));
+                }
+            }
+            if (p.diag & FC_DIAG_HIST) {
+                if (is_acc) {
+                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
+                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb_after], (unsigned long long)run_len);
+                }
+                if (lane == 0 && r0) {
+                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut0], (unsigned long long)r0);
+                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb0], (unsigned long long)r0);
+                }
+            }
+            if (p.diag & FC_DIAG_FLIPS) {
+                // part.flips is stale on rejected steps: every yield of a run repeats the update
+                // for the node whose flip created the state (grid_chain_sec11.py:396-400).
+                int64_t *nf = p.num_flips + (size_t)c * n, *ps = p.part_sum + (size_t)c * n;
+                unsigned long long *lf = (unsigned long long *)(p.last_flipped + (size_t)c * n);
+                if (lane == 0 && r0 && last_flip0 >= 0) {
+                    const int64_t t_last = steps0 + r0;
+                    const int64_t old = (int64_t)atomicExch(lf + last_flip0, (unsigned long long)t_last);
+                    atomicAdd((unsigned long long *)(ps + last_flip0), (unsigned long long)(-(int64_t)p.labels[a_last0] * (t_last - old)));
+                    atomicAdd((unsigned long long *)(nf + last_flip0), (unsigned long long)r0);
+                }
+                __builtin_amdgcn_s_waitcnt(0);
+                if (is_acc) {
+                    const int64_t t_last = t_acc + run_len - 1;
+                    const int64_t old = (int64_t)atomicExch(lf + v, (unsigned long long)t_last);
+                    atomicAdd((unsigned long long *)(ps + v), (unsigned long long)(-(int64_t)p.labels[tgt] * (t_last - old)));
+                    atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
+                }
+            }
+            if ((p.diag & FC_DIAG_EDGES) && is_acc) {
+                int64_t *ea = p.edge_acc + (size_t)c * p.n_edges;
+                unsigned long long *es = (unsigned long long *)(p.edge_since + (size_t)c * p.n_edges);
+                for (int i = 0; i < RMAX; ++i) {
+                    if (!((nbr >> i) & 1u)) continue;
+                    const int e = p.ring_eid[(size_t)v * RMAX + i];
+                    if ((inA >> i) & 1u) {
+                        atomicExch(es + e, (unsigned long long)t_acc);             // becomes cut
+                    } else if ((tmask >> i) & 1u) {
+                        const int64_t since = (int64_t)atomicAdd(es + e, 0ull);    // becomes uncut
+                        atomicAdd((unsigned long long *)(ea + e), (unsigned long long)(t_acc - since));
+                    }
+                }
+            }
+            if (trace_on) {
+                const uint64_t PM = __ballot(hit && done);
+                const uint64_t mine = ACCM & bits_below(lane + 1);
+                const int src = mine ? 63 - __builtin_clzll(mine) : 0;
+                const int c_j = __shfl(cut_after, src), n_j = __shfl(nb_after, src);
+                const long long w_j = __shfl((long long)my_wait, src);
+                const int64_t idx = trace_len + __popcll(PM & bits_below(lane));
+                if (hit && done && idx < p.trace_cap) {
+                    fc_record &rr = p.trace[(size_t)c * p.trace_cap + idx];
+                    const bool valid = (st & ST_VS) != 0;
+                    rr.draw = (int64_t)d;
+                    rr.v = v;
+                    rr.flags = (valid ? (1 | (is_acc ? 2 : 0)) : ((st & ST_IC) ? 4 : 8)) | (tgt << 8);
+                    rr.cut = mine ? c_j : cut0;
+                    rr.nb = mine ? n_j : nb0;
+                    rr.wait = valid ? (mine ? (int64_t)w_j : wait_cur) : 0;
+                }
+                trace_len += __popcll(PM);
+            }
+        }
+        if (ACCM) {
+            const int la = 63 - __builtin_clzll(ACCM);
+            wait_cur = (int64_t)(((uint64_t)(uint32_t)rl32((int)(uint32_t)my_wait, la)) |
+                                 ((uint64_t)(uint32_t)rl32((int)(my_wait >> 32), la) << 32));
+        }
+        // draws consumed by the committed slots [0, end)
+        int consumed;
+        if (target_hit) {
+            consumed = rl32(off_l, end - 1) + 1;
+        } else {
+            consumed = end < ns ? rl32(off_l, end) : gen;
+            if (trunc_off < consumed) consumed = trunc_off;
+        }
+        draw += (uint64_t)consumed;
+        compiler_fence();
+        FC_STAMP(t_e);
+        FC_PROF(4, t_e - t_d);
+    }
+    FC_STAMP(t_loop1);
+    FC_PROF(0, t_loop1 - t_loop0);
+#ifdef FC_PHASE_PROF
+    if (p.prof && lane == 0)
+        for (int i = 0; i < kProfSlots; ++i) p.prof[(size_t)c * kProfSlots + i] = prof_acc[i];
+#endif
+
+    // ---- write back ---------------------------------------------------------------------
+    {
+        uint4 *ga = (uint4 *)(p.assign + (size_t)c * npad);
+        uint4 *gf = (uint4 *)(p.fcnt + (size_t)c * npad);
+        for (int i = lane; i < npad / 16; i += kWave) {
+            ga[i] = ((const uint4 *)a)[i];
+            gf[i] = ((const uint4 *)fcnt)[i];
+        }
+    }
+    int64_t cnt_prop = n_prop, cnt_acc = n_acc, cnt_ic = n_ic, cnt_ip = n_ip;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        acc_cut += __shfl_xor((long long)acc_cut, off);
+        acc_nb += __shfl_xor((long long)acc_nb, off);
+        acc_wait += __shfl_xor((long long)acc_wait, off);
+        acc_cut2 += __shfl_xor((long long)acc_cut2, off);
+        acc_nb2 += __shfl_xor((long long)acc_nb2, off);
+        cnt_prop += __shfl_xor((long long)cnt_prop, off);
+        cnt_acc += __shfl_xor((long long)cnt_acc, off);
+        cnt_ic += __shfl_xor((long long)cnt_ic, off);
+        cnt_ip += __shfl_xor((long long)cnt_ip, off);
+    }
+    if (lane == 0) {
+        scp->draw = draw;
+        scp->steps = steps;
+        scp->proposals += cnt_prop;
+        scp->accepted += cnt_acc;
+        scp->inv_contig += cnt_ic;
+        scp->inv_pop += cnt_ip;
+        scp->bfs_calls = bfs_calls;
+        scp->bfs_levels = bfs_levels;
+        if (FULL) {
+            scp->trace_len = trace_len;
+            scp->ev_len = ev_len;
+            scp->hit_time = hit_time;
+        }
+        scp->sum_cut += acc_cut;
+        scp->sum_nb += acc_nb;
+        scp->sum_wait += acc_wait;
+        scp->sum_cut2 += acc_cut2;
+        scp->sum_nb2 += acc_nb2;
+        scp->cut = cut;
+        scp->nb = nb;
+        scp->pops[0] = pops0;
+        scp->pops[1] = pops1;
+        scp->ngamma[0] = ng0;
+        scp->ngamma[1] = ng1;
+        scp->wait_cur = wait_cur;
+        scp->last_flip = last_flip;
+        scp->stuck = stuck;
+    }
+}
+
+int launch_flip2(const KParams &p, int ring_max, void *stream) {
+    const int wpb = waves_per_block(p.chain_lds_bytes);
+    const int blocks = (p.n_chains + wpb - 1) / wpb;
+    const size_t lds = (size_t)p.chain_lds_bytes * wpb;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(blocks), block(kWave * wpb);
+    // FULL: replay tapes, traces, event logs, histograms, per-node/per-edge tallies or a
+    // hitting-time window; the lean instance keeps its registers for the hot loop.
+    const bool full = p.tape || p.trace || (p.diag & ~(uint32_t)FC_DIAG_WAIT) || p.hit_lo <= p.hit_hi;
+#define FC_LAUNCH2(R, S, F)                                                                             \
+    do {                                                                                                \
+        if (lds > 65536)                                                                                \
+            (void)hipFuncSetAttribute((const void *)flip2_kernel<R, S, F>,                              \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
+        hipLaunchKernelGGL((flip2_kernel<R, S, F>), grid, block, lds, s, p);                            \
+    } while (0)
+#define FC_FULL2(R, S)                   \
+    do {                                 \
+        if (full) FC_LAUNCH2(R, S, true);  \
+        else FC_LAUNCH2(R, S, false);      \
+    } while (0)
+#define FC_NSUB2(R)                                \
+    switch (p.nsub) {                              \
+        case 1: FC_FULL2(R, 1); break;             \
+        case 2: FC_FULL2(R, 2); break;             \
+        case 4: FC_FULL2(R, 4); break;             \
+        default: return (int)hipErrorInvalidValue; \
+    }
+    if (ring_max == 8) {
+        FC_NSUB2(8)
+    } else if (ring_max == 16) {
+        FC_NSUB2(16)
+    } else {
+        return (int)hipErrorInvalidValue;
+    }
+#undef FC_NSUB2
+#undef FC_FULL2
+#undef FC_LAUNCH2
+    return (int)hipGetLastError();
+}
+
+}  // namespace fc

@@ -113,10 +113,19 @@ struct KParams {
     int32_t hit_lo, hit_hi;     // hitting-time window on |cut| (lo > hi: off)
     int32_t nsub;               // max draw rounds of 64 per batch (1, 2, 4)
     int32_t hit_stop;           // start another round only while fewer boundary hits than this
+    int64_t *prof;              // [n_chains * kProfSlots] phase cycles (FC_PHASE_PROF builds only)
+    int32_t par_min;            // k = 2: segment-parallel commit from this many acceptances on
 };
 
+// Diagnostic build (-DFC_PHASE_PROF): s_memtime cycles per kernel phase, per chain.
+// slots: 0 loop total, 1 draws, 2 evaluate, 3 commit, 4 bookkeeping, 5 batches,
+//        6 commit-loop iterations, 7 applied flips; k = 2 commit detail: 8 verdicts,
+//        9 one-event classify, 10 one-event apply, 11 segment-parallel, 12 segments
+constexpr int kProfSlots = 16;
+
 // Launch wrappers (fc_kernels.hip).  Return a hipError_t as int.
-int launch_flip_k2(const KParams &p, int ring_max, void *stream);
+int launch_flip_k2(const KParams &p, int ring_max, void *stream);   // k > 2 (fc_kernels.hip)
+int launch_flip2(const KParams &p, int ring_max, void *stream);     // k = 2 (fc_flip2.hip)
 int launch_init_fcnt(const KParams &p, int ring_max, void *stream);
 
 // Series diagnostics (fc_series.hip): expand the event logs of chains [c0, c0 + nc) into

@@ -25,117 +25,15 @@
 
 #include "fc_internal.h"
 #include "fc_philox.h"
+#include "fc_device.h"
 
 namespace fc {
 
-namespace {
-
-// LDS operations of one wave execute in order; the fence only stops the compiler moving
-// LDS accesses across it.  Full waits (wave_sync) are used where lanes hand data to each
-// other through atomics (BFS).
-__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
-__device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-__device__ __forceinline__ uint64_t bits_below(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
-__device__ __forceinline__ uint64_t lane_range(int lo, int hi) { return bits_below(hi) & ~bits_below(lo); }
-
-__device__ __forceinline__ int rl32(int x, int lane) { return __builtin_amdgcn_readlane(x, lane); }
-__device__ __forceinline__ uint32_t rlu(uint32_t x, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)x, lane); }
-
-__device__ __forceinline__ int kth_set_bit(uint64_t x, int k) {  // k >= 1
-    for (int i = 1; i < k; ++i) x &= x - 1;
-    return __builtin_ctzll(x);
-}
-
-template <int RMAX>
-__device__ __forceinline__ int ring_entry(const uint32_t (&ring)[RMAX / 2], int i) {
-    return (int)((ring[i >> 1] >> (16 * (i & 1))) & 0xffffu);
-}
-
-// At most one of the cyclic intervals between consecutive old-district neighbours holds a
-// break (a ring step that is not an old-district link) <=> the neighbours form one run.
-__device__ __forceinline__ bool one_run(uint32_t nbrA, uint32_t brk, uint32_t full) {
-    if (__popc(nbrA) <= 1) return true;
-    uint32_t cur = nbrA & (0u - nbrA);
-    uint32_t rest = nbrA & (nbrA - 1u);
-    int cnt = 0;
-    while (rest) {
-        const uint32_t nx = rest & (0u - rest);
-        cnt += (brk & (nx - cur)) != 0u;
-        cur = nx;
-        rest &= rest - 1u;
-    }
-    const uint32_t first = nbrA & (0u - nbrA);  // wrap interval [cur, L) U [0, first)
-    cnt += (brk & ((full & ~(cur - 1u)) | (first - 1u))) != 0u;
-    return cnt <= 1;
-}
-
-// Wave-cooperative BFS over the old district with v removed: are all old-district
-// neighbours of v (each lane < RMAX may hold one as its target) connected to `start`?
-template <int RMAX>
-__device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, uint64_t *vis, uint64_t *front,
-                         uint64_t *nxt, int words, int lane, int vf, int A, int my_target, int start,
-                         int64_t &levels) {
-    for (int i = lane; i < words; i += kWave) {
-        vis[i] = 0;
-        front[i] = 0;
-        nxt[i] = 0;
-    }
-    wave_sync();
-    if (lane == 0) {
-        vis[vf >> 6] |= 1ull << (vf & 63);
-        vis[start >> 6] |= 1ull << (start & 63);
-        front[start >> 6] |= 1ull << (start & 63);
-    }
-    wave_sync();
-    for (;;) {
-        ++levels;
-        for (int i = lane; i < words; i += kWave) {
-            uint64_t bits = front[i];
-            while (bits) {
-                const int b = __builtin_ctzll(bits);
-                bits &= bits - 1;
-                const NodeRec<RMAX> r = G[i * 64 + b];
-                const uint32_t nbr = (uint32_t)(r.meta >> kMetaNbrShift) & 0xffffu;
-#pragma unroll
-                for (int j = 0; j < RMAX; ++j) {
-                    if (!((nbr >> j) & 1u)) continue;
-                    const int e = ring_entry<RMAX>(r.ring, j);
-                    if (a[e] != A) continue;
-                    const uint64_t bit = 1ull << (e & 63);
-                    const uint64_t old = atomicOr((unsigned long long *)&vis[e >> 6], (unsigned long long)bit);
-                    if (!(old & bit)) atomicOr((unsigned long long *)&nxt[e >> 6], (unsigned long long)bit);
-                }
-            }
-        }
-        wave_sync();
-        const bool found = my_target < 0 || ((vis[my_target >> 6] >> (my_target & 63)) & 1ull);
-        if (__all(found)) return true;
-        bool any = false;
-        for (int i = lane; i < words; i += kWave) {
-            const uint64_t x = nxt[i];
-            front[i] = x;
-            nxt[i] = 0;
-            any |= x != 0;
-        }
-        wave_sync();
-        if (!__any(any)) return false;
-    }
-}
-
-// per-lane status bits of the slots of one batch
-constexpr uint32_t ST_VS = 1u;   // valid step
-constexpr uint32_t ST_AC = 2u;   // accepted
-constexpr uint32_t ST_IC = 4u;   // invalid: contiguity
-constexpr uint32_t ST_IP = 8u;   // invalid: population
-constexpr uint32_t ST_BD = 16u;  // contiguity resolved by BFS
-constexpr uint32_t ST_BR = 32u;  // ... and its result
-
-}  // namespace
+using namespace dev;
 
 // KM = 2: two districts (BI_SIGN, and PAIR with k = 2, which coincide); the outer-face
 // exact rule applies.  KM = 0: k <= 32 districts, PAIR proposals, populations in LDS.
-template <int RMAX, int NSUB, int KM>
+template <int RMAX, int NSUB, int KM, bool FULL>
 __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
@@ -181,18 +79,24 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     int stuck = 0;
     int rem = (int)p.n_steps;  // steps still to take in this launch (host: n_steps < 2^31)
     uint64_t draw_cap = draw + (uint64_t)p.max_draws;
-    if (p.tape && draw_cap > (uint64_t)p.tape_draws) draw_cap = (uint64_t)p.tape_draws;
+    if (FULL && p.tape && draw_cap > (uint64_t)p.tape_draws) draw_cap = (uint64_t)p.tape_draws;
     const uint32_t chain_gid = p.chain_id_offset + (uint32_t)c;
     const bool force_bfs = (p.flags & FC_FLAG_FORCE_BFS) != 0;
     const bool want_wait = (p.diag & FC_DIAG_WAIT) != 0;
-    const bool trace_on = p.trace && c < p.trace_chains;
+    const bool trace_on = FULL && p.trace && c < p.trace_chains;
 
     // per-lane accumulators, reduced once per launch
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
     uint32_t n_prop = 0, n_acc = 0, n_ic = 0, n_ip = 0;
+#ifdef FC_PHASE_PROF
+    int64_t prof_acc[kProfSlots] = {};
+#endif
     wave_sync();
+    FC_STAMP(t_loop0);
 
     while (rem > 0) {
+        FC_STAMP(t_a);
+        FC_PROF(5, 1);
         if (draw >= draw_cap) {
             stuck = 1;
             break;
@@ -212,7 +116,7 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
             const bool inrange = (uint64_t)off < room;
             const uint64_t dr = draw + (uint64_t)off;
             Words4 w;
-            if (p.tape) {
+            if (FULL && p.tape) {
                 const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + (inrange ? dr : draw)) * 6;
                 w = Words4{t[0], t[1], t[2], t[3]};
             } else {
@@ -246,6 +150,8 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
         }
         const int ns = nh < 64 ? nh : 64;
         compiler_fence();
+        FC_STAMP(t_b);
+        FC_PROF(1, t_b - t_a);
 
         // ---- 1b. evaluate every slot against the current state ---------------------------
         const bool has = lane < ns;
@@ -356,6 +262,8 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
         const uint32_t pk = (uint32_t)v | ((uint32_t)av << 15) | ((uint32_t)tgt << 21) | ((uint32_t)gam << 27);
         const uint32_t pk2 = inA | (nbr << 16);
         const uint32_t pk3 = tmask | ((uint32_t)(delta + 32) << 16);  // |delta| <= deg <= 16
+        FC_STAMP(t_c);
+        FC_PROF(2, t_c - t_b);
 
         // ---- 2. commit loop (wave-uniform) -----------------------------------------------
         uint32_t st = 0;
@@ -367,20 +275,39 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
         const int last_flip0 = last_flip;
         const int a_last0 = last_flip0 >= 0 ? (int)a[last_flip0] : 0;
         int cut_after = 0, nb_after = 0;
+        // contiguity undecided by the ring rule at slot f: wave BFS on the current state
+        auto run_bfs = [&](int f) -> bool {
+            const uint32_t pkf = rlu(pk, f), nbrAf = rlu(pk2, f) & rlu(pk2, f) >> 16;
+            int my_target = -1, start = -1;
+#pragma unroll
+            for (int k2 = 0; k2 < RMAX / 2; ++k2) {
+                const uint32_t wrd = rlu(rec.ring[k2], f);
+                if ((lane >> 1) == k2) my_target = (int)((wrd >> (16 * (lane & 1))) & 0xffffu);
+                if (start < 0 && ((nbrAf >> (2 * k2)) & 1u)) start = (int)(wrd & 0xffffu);
+                if (start < 0 && ((nbrAf >> (2 * k2 + 1)) & 1u)) start = (int)(wrd >> 16);
+            }
+            if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
+            ++bfs_calls;
+            return wave_bfs<RMAX>(G, a, vis, front, nxt, p.words, lane, (int)(pkf & 0x7fffu),
+                                  (int)((pkf >> 15) & 63u), my_target, start, bfs_levels);
+        };
         while (pos < end) {
-            bool known = true, ok;
+            FC_PROF(6, 1);
+            const bool prop = isprop && lane >= pos && lane < end;
+            // contiguity verdict when the other district does / does not touch the outer face
+            bool known = true, okT, okN;
             if (st & ST_BD) {
-                ok = (st & ST_BR) != 0;
+                okT = okN = (st & ST_BR) != 0;
             } else if (nA == 0) {
-                ok = false;
+                okT = okN = false;
             } else if (exact) {
-                const bool touch = (av ? ng0 : ng1) > 0;  // the other district touches the outer face
-                ok = (gam && !touch) ? s_cyc : s_lin;
+                okT = s_lin;
+                okN = gam ? s_cyc : s_lin;
             } else if (KM == 0 && s_cut) {
-                ok = false;
+                okT = okN = false;
             } else {
                 known = s_lin;
-                ok = s_lin;
+                okT = okN = s_lin;
             }
             int pa, pb;
             if constexpr (KM == 2) {
@@ -390,9 +317,10 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
                 pa = popk[av];
                 pb = popk[tgt];
             }
+            const bool ok = ((av ? ng0 : ng1) > 0) ? okT : okN;
             const bool popok = (pa - pv >= p.pop_lo) && (pb + pv <= p.pop_hi);
-            const bool prop = isprop && lane >= pos && lane < end;
             const bool valid = prop && known && ok && popok;
+            // ---- one event at a time: the first acceptance or undecided slot -----------------
             const uint64_t VAL = __ballot(valid);
             const uint64_t EV = __ballot((valid && acc) || (prop && !known));
             const int f = EV ? __builtin_ctzll(EV) : end;
@@ -413,23 +341,12 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
             if (f >= end) break;
             if (!((VAL >> f) & 1ull)) {
                 // undecided contiguity at slot f: device BFS on the current state
-                const uint32_t pkf = rlu(pk, f), nbrAf = rlu(pk2, f) & rlu(pk2, f) >> 16;
-                int my_target = -1, start = -1;
-#pragma unroll
-                for (int k2 = 0; k2 < RMAX / 2; ++k2) {
-                    const uint32_t wrd = rlu(rec.ring[k2], f);
-                    if ((lane >> 1) == k2) my_target = (int)((wrd >> (16 * (lane & 1))) & 0xffffu);
-                    if (start < 0 && ((nbrAf >> (2 * k2)) & 1u)) start = (int)(wrd & 0xffffu);
-                    if (start < 0 && ((nbrAf >> (2 * k2 + 1)) & 1u)) start = (int)(wrd >> 16);
-                }
-                if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
-                const bool res = wave_bfs<RMAX>(G, a, vis, front, nxt, p.words, lane, (int)(pkf & 0x7fffu),
-                                                (int)((pkf >> 15) & 63u), my_target, start, bfs_levels);
-                ++bfs_calls;
+                const bool res = run_bfs(f);
                 if (lane == f) st |= ST_BD | (res ? ST_BR : 0u);
                 continue;
             }
             // ---- accept slot f: apply the flip -----------------------------------------
+            FC_PROF(7, 1);
             const uint32_t pkf = rlu(pk, f), pk2f = rlu(pk2, f), pk3f = rlu(pk3, f);
             const int vf = (int)(pkf & 0x7fffu), Af = (int)((pkf >> 15) & 63u), tf = (int)((pkf >> 21) & 63u);
             const bool gamf = (pkf >> 27) & 1u;
@@ -522,6 +439,8 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
             if (trunc_off < consumed) consumed = trunc_off;
         }
         steps = steps0 + (rem0 - rem);
+        FC_STAMP(t_d);
+        FC_PROF(3, t_d - t_c);
 
         // ---- 3. lane-parallel bookkeeping of the committed batch ----------------------------
         const bool done = lane < end;
@@ -540,7 +459,7 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
         int64_t my_wait = 0;
         if (want_wait && is_acc) {
             Words4 g;
-            if (p.tape) {
+            if (FULL && p.tape) {
                 const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + d) * 6;
                 g = Words4{t[4], t[5], 0u, 0u};
             } else {
@@ -564,7 +483,7 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
             acc_wait += wait_cur * r0;
         }
         const int64_t t_acc = steps0 + __popcll(VSM & bits_below(lane + 1));  // yield index of this slot
-        if ((p.diag & FC_DIAG_SERIES) && ACCM) {
+        if (FULL && (p.diag & FC_DIAG_SERIES) && ACCM) {
             const int64_t idx = ev_len + __popcll(ACCM & bits_below(lane));
             if (is_acc && idx < p.ev_cap) {
                 fc_event ev;
@@ -578,11 +497,11 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
             }
             ev_len += __popcll(ACCM);
         }
-        if (hit_time < 0 && ACCM) {
+        if (FULL && hit_time < 0 && ACCM) {
             const uint64_t hm = __ballot(is_acc && cut_after >= p.hit_lo && cut_after <= p.hit_hi);
             if (hm) hit_time = (int64_t)__shfl((long long)t_acc, __builtin_ctzll(hm));
         }
-        if (p.diag & (FC_DIAG_HIST | FC_DIAG_FLIPS | FC_DIAG_EDGES)) {
+        if (FULL && (p.diag & (FC_DIAG_HIST | FC_DIAG_FLIPS | FC_DIAG_EDGES))) {
             if (p.diag & FC_DIAG_HIST) {
                 if (is_acc) {
                     atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
@@ -649,7 +568,15 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
         if (ACCM) wait_cur = (int64_t)__shfl((long long)my_wait, 63 - __builtin_clzll(ACCM));
         draw += (uint64_t)consumed;
         compiler_fence();
+        FC_STAMP(t_e);
+        FC_PROF(4, t_e - t_d);
     }
+    FC_STAMP(t_loop1);
+    FC_PROF(0, t_loop1 - t_loop0);
+#ifdef FC_PHASE_PROF
+    if (p.prof && lane == 0)
+        for (int i = 0; i < kProfSlots; ++i) p.prof[(size_t)c * kProfSlots + i] = prof_acc[i];
+#endif
 
     // ---- write back ---------------------------------------------------------------------
     {
@@ -709,28 +636,37 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream) {
     const size_t lds = (size_t)p.chain_lds_bytes * wpb;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(blocks), block(kWave * wpb);
-#define FC_LAUNCH(R, S, K)                                                                              \
+    // FULL: replay tapes, traces, event logs, histograms, per-node/per-edge tallies or a
+    // hitting-time window; the lean instance (proposals, steps, sums, waits) keeps its
+    // register budget for the hot loop.
+    const bool full = p.tape || p.trace || (p.diag & ~(uint32_t)FC_DIAG_WAIT) || p.hit_lo <= p.hit_hi;
+#define FC_LAUNCH(R, S, K, F)                                                                           \
     do {                                                                                                \
         if (lds > 65536)                                                                                \
-            (void)hipFuncSetAttribute((const void *)flip_kernel<R, S, K>,                               \
+            (void)hipFuncSetAttribute((const void *)flip_kernel<R, S, K, F>,                            \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
-        hipLaunchKernelGGL((flip_kernel<R, S, K>), grid, block, lds, s, p);                             \
+        hipLaunchKernelGGL((flip_kernel<R, S, K, F>), grid, block, lds, s, p);                          \
+    } while (0)
+#define FC_FULL_SWITCH(R, S, K)                          \
+    do {                                                 \
+        if (full) FC_LAUNCH(R, S, K, true);              \
+        else FC_LAUNCH(R, S, K, false);                  \
     } while (0)
 #define FC_NSUB_SWITCH(R, K)                          \
     switch (p.nsub) {                                 \
-        case 1: FC_LAUNCH(R, 1, K); break;            \
-        case 2: FC_LAUNCH(R, 2, K); break;            \
-        case 4: FC_LAUNCH(R, 4, K); break;            \
+        case 1: FC_FULL_SWITCH(R, 1, K); break;       \
+        case 2: FC_FULL_SWITCH(R, 2, K); break;       \
         default: return (int)hipErrorInvalidValue;    \
     }
     if (ring_max == 8) {
-        if (p.k == 2) { FC_NSUB_SWITCH(8, 2) } else { FC_NSUB_SWITCH(8, 0) }
+        FC_NSUB_SWITCH(8, 0)
     } else if (ring_max == 16) {
-        if (p.k == 2) { FC_NSUB_SWITCH(16, 2) } else { FC_NSUB_SWITCH(16, 0) }
+        FC_NSUB_SWITCH(16, 0)
     } else {
         return (int)hipErrorInvalidValue;
     }
 #undef FC_NSUB_SWITCH
+#undef FC_FULL_SWITCH
 #undef FC_LAUNCH
     return (int)hipGetLastError();
 }

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
 TAG=${1:-r01}
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > "$OUT/pytest_gpu_$TAG.log" 2>&1 || { echo "pytest failed"; tail -40 "$OUT/pytest_gpu_$TAG.log"; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1 || { echo "pytest failed"; tail -40 "$OUT/pytest_gpu_$TAG.log"; exit 1; }
 tail -3 "$OUT/pytest_gpu_$TAG.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1 || { echo "smoke failed"; tail -40 "$OUT/smoke_$TAG.log"; exit 1; }
 tail -2 "$OUT/smoke_$TAG.log"

@@ -1,0 +1,25 @@
+"""Summarise FC_PROF_OUT dumps of the FC_PHASE_PROF build: per base group (chain % groups),
+mean per-chain s_memtime cycles per phase of the last launch, per batch and per applied flip.
+usage: python tools/prof_report.py FILE n_chains [groups]"""
+import sys
+import numpy as np
+f, C = sys.argv[1], int(sys.argv[2])
+G = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+raw = np.fromfile(f, dtype=np.int64)
+S = raw.size // C // (raw.size // C // 8 if False else 1)
+S = 16 if (raw.size // C) % 16 == 0 else 8
+rec = raw.reshape(-1, C, S)
+last = rec[-1].astype(np.float64)
+names = ["total", "draws", "eval", "commit", "book", "batches", "commit_it", "applied"]
+print("grp  total_Mcyc  batches  applied  commit_it | per batch: draws  eval  commit  book | commit/applied")
+for g in range(G):
+    x = last[np.arange(C) % G == g].mean(axis=0)
+    b = max(x[5], 1)
+    print(f"{g:3d}  {x[0]/1e6:9.2f}  {x[5]:8.0f} {x[7]:8.0f} {x[6]:9.0f} | {x[1]/b:8.0f} {x[2]/b:5.0f} {x[3]/b:7.0f} {x[4]/b:5.0f} | {x[3]/max(x[7],1):8.0f}")
+if S == 16:
+    print("grp | per iteration: verdict | one-event classify/apply per applied | parallel per segment, segments/batch")
+    for g in range(G):
+        x = last[np.arange(C) % G == g].mean(axis=0)
+        it = max(x[6], 1)
+        print(f"{g:3d} | {x[8]/it:8.0f} | {x[9]/max(x[7],1):8.0f} {x[10]/max(x[7],1):8.0f} | {x[11]/max(x[12],1):8.0f} {x[12]/max(x[5],1):6.2f}")
+print("max chain total Mcyc", last[:, 0].max() / 1e6, "argmax", int(last[:, 0].argmax()))
