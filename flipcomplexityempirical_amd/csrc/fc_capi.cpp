@@ -242,6 +242,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + 3 * r->words * 8 + 5 * 64 * 4 + fc::kMaxKGeneral * 4;
     r->wmax = 1;
     if (k > 2) r->wmax = p->wmax > 0 ? p->wmax : std::max(1, std::min(g.max_degree, k - 1));
+#ifdef FC_PHASE_PROF
+    r->chain_lds_bytes += fc::kProfSlots * 8;  // phase-cycle accumulators (diagnostic build)
+#endif
     r->chain_lds_bytes = (r->chain_lds_bytes + 15) & ~15;
     if ((size_t)r->chain_lds_bytes * fc::waves_per_block(r->chain_lds_bytes) > 160 * 1024)
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: graph too large for the wave-per-chain LDS layout");

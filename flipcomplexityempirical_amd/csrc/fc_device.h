@@ -16,7 +16,9 @@ __device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)
 
 #ifdef FC_PHASE_PROF
 #define FC_STAMP(t) const int64_t t = (int64_t)__builtin_amdgcn_s_memtime()
-#define FC_PROF(i, x) (prof_acc[i] += (int64_t)(x))
+// accumulators live in the chain's LDS tail (prof_acc), so profiling adds no registers
+#define FC_PROF(i, x) \
+    do { if (lane == 0) atomicAdd((unsigned long long *)&prof_acc[i], (unsigned long long)(int64_t)(x)); } while (0)
 #else
 #define FC_STAMP(t)
 #define FC_PROF(i, x)
@@ -138,6 +140,15 @@ constexpr uint32_t ST_IC = 4u;   // invalid: contiguity
 constexpr uint32_t ST_IP = 8u;   // invalid: population
 constexpr uint32_t ST_BD = 16u;  // contiguity resolved by BFS
 constexpr uint32_t ST_BR = 32u;  // ... and its result
+// per-slot predicates of the k = 2 kernel, packed beside the status bits
+constexpr uint32_t LF_HIT = 1u << 8;     // proposal (boundary node)
+constexpr uint32_t LF_ACC = 1u << 9;     // Metropolis test passed
+constexpr uint32_t LF_SLIN = 1u << 10;   // run rule, open ring
+constexpr uint32_t LF_SCYC = 1u << 11;   // run rule, ring closed through the outer face
+constexpr uint32_t LF_EXACT = 1u << 12;  // the run rule decides contiguity exactly
+constexpr uint32_t LF_GAM = 1u << 13;    // outer-face node
+constexpr uint32_t LF_HAS = 1u << 14;    // the lane holds a slot
+constexpr uint32_t LF_WROTE = 1u << 15;  // the lane holds commit marks
 
 }  // namespace dev
 }  // namespace fc

@@ -89,7 +89,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
     uint32_t n_prop = 0, n_acc = 0, n_ic = 0, n_ip = 0;
 #ifdef FC_PHASE_PROF
-    int64_t prof_acc[kProfSlots] = {};
+    int64_t *prof_acc = (int64_t *)(base + p.chain_lds_bytes - kProfSlots * 8);
+    if (lane < kProfSlots) prof_acc[lane] = 0;
 #endif
     wave_sync();
     FC_STAMP(t_loop0);
@@ -150,16 +151,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
 
         // ---- 2. every slot against the current state --------------------------------------
         const bool has = lane < ns;
-        const int off_l = has ? (int)slot[192 + lane] : gen;
+        int off_l = has ? (int)slot[192 + lane] : gen;
         const uint64_t d = draw + (uint64_t)off_l;
-        const int v = has ? (int)slot[lane] : 0;
+        int v = has ? (int)slot[lane] : 0;
         const uint32_t w1 = slot[64 + lane], w2 = slot[128 + lane];
         const NodeRec<RMAX> rec = G[v];
-        const int av = a[v];
-        const int pv = rec.pop;
+        int av = a[v];
+        int pv = rec.pop;
         const uint32_t Ln = (uint32_t)(rec.meta & kMetaLenMask);
         const uint32_t full = (1u << Ln) - 1u;
-        const uint32_t nbr = (uint32_t)(rec.meta >> kMetaNbrShift) & 0xffffu;
+        uint32_t nbr = (uint32_t)(rec.meta >> kMetaNbrShift) & 0xffffu;
         const uint32_t link = (uint32_t)(rec.meta >> kMetaLinkShift) & 0xffffu;
         int cell[RMAX];  // ring cells (padded with the node itself)
         uint32_t inA = 0;
@@ -171,9 +172,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         inA &= full;
         const int tgt = 1 - av;                 // -1 * assignment, grid_chain_sec11.py:145
         const uint32_t nbrA = inA & nbr;        // old-district neighbours
-        const uint32_t tmask = nbr & ~inA;      // target-district neighbours
-        const int nA = __popc(nbrA);
-        const int delta = nA - __popc(tmask);   // cut(S') - cut(S)
+        uint32_t tmask = nbr & ~inA;            // target-district neighbours
+        int nA = __popc(nbrA);
+        int delta = nA - __popc(tmask);         // cut(S') - cut(S)
         const bool hit = has && tmask != 0u;    // v in b_nodes: a proposal
         bool s_lin, s_cyc;
         {
@@ -186,11 +187,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         const bool exact = (rec.meta & kMetaExact) && !force_bfs;
         const bool gam = (rec.meta & kMetaGamma) != 0;
         const bool acc = mant53(w1, w2) < T[delta + RMAX];
+        // per-slot predicates live as bits of one VGPR (st) through the commit; the compiler
+        // would otherwise hold each as a 64-bit lane mask in SGPRs for the whole loop
+        uint32_t st = (hit ? LF_HIT : 0u) | (acc ? LF_ACC : 0u) | (s_lin ? LF_SLIN : 0u) | (s_cyc ? LF_SCYC : 0u) |
+                      (exact ? LF_EXACT : 0u) | (gam ? LF_GAM : 0u) | (has ? LF_HAS : 0u);
         FC_STAMP(t_c);
         FC_PROF(2, t_c - t_b);
 
         // ---- 3. commit in draw order ----------------------------------------------------
-        uint32_t st = 0;
         int end = ns, pos = 0;
         int trunc_off = gen;  // first draw offset not consumed by this batch
         bool target_hit = false;
@@ -201,7 +205,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         int cut_after = 0, nb_after = 0;
         const int dp_l = av == 0 ? -pv : pv;            // pops0 change of this lane's flip
         const int dg_l = gam ? (av == 0 ? -1 : 1) : 0;  // ngamma0 change
-        bool wrote = false;                              // this lane holds commit marks
 
         // contiguity undecided by the ring rule at lane f: wave BFS on the current state
         auto run_bfs = [&](int f) -> bool {
@@ -222,6 +225,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
 
         while (pos < end) {
             FC_PROF(6, 1);
+            // re-derive the predicates each iteration: loop-invariant lane values would otherwise
+            // be hoisted as lane masks into SGPRs and spilled
+            asm volatile("" : "+v"(st), "+v"(inA), "+v"(tmask), "+v"(nbr), "+v"(delta), "+v"(nA), "+v"(av), "+v"(pv),
+                         "+v"(v), "+v"(off_l));
+            const bool hit = (st & LF_HIT) != 0, acc = (st & LF_ACC) != 0, s_lin = (st & LF_SLIN) != 0,
+                       s_cyc = (st & LF_SCYC) != 0, exact = (st & LF_EXACT) != 0, gam = (st & LF_GAM) != 0,
+                       has = (st & LF_HAS) != 0;
             const bool prop = hit && lane >= pos && lane < end;
             // contiguity verdict when the other district does (okT) / does not (okN) touch
             // the outer face -- the outer-face counts are chain-global
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 int x = kWave;  // first lane that must not be committed
                 if (K) {
                     const bool inK = (K >> lane) & 1ull;
-                    wrote |= inK;
+                    if (inK) st |= LF_WROTE;
                     // marks: smark[node] / nmark[neighbour] = lowest candidate lane (0xff: none)
                     bool need = inK;
                     int ms, mn[RMAX];
@@ -350,9 +360,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
 #pragma unroll
                     for (int i = 0; i < RMAX; ++i) {
                         const bool nb_i = me && ((nbr >> i) & 1u);
-                        const int dlt = (int)((inA >> i) & 1u) - (int)((tmask >> i) & 1u);
-                        *(nb_i ? &fcnt[cell[i]] : dum) = (uint8_t)(oldc[i] + dlt);
-                        dnb += nb_i ? (int)(dlt > 0 && oldc[i] == 0) - (int)(dlt < 0 && oldc[i] == 1) : 0;
+                        const uint32_t up = (inA >> i) & 1u, dn = (tmask >> i) & 1u;  // dlt = up - dn
+                        *(nb_i ? &fcnt[cell[i]] : dum) = (uint8_t)(oldc[i] + (int)up - (int)dn);
+                        dnb += nb_i ? (int)(up & (uint32_t)(oldc[i] == 0)) - (int)(dn & (uint32_t)(oldc[i] == 1)) : 0;
                     }
                     *(me ? (uint8_t *)&a[v] : dum) = (uint8_t)tgt;
                     *(me ? &fcnt[v] : dum) = (uint8_t)nA;
@@ -495,7 +505,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 break;
             }
         }
-        if (wrote) {  // clear this lane's marks for the next batch
+        if (st & LF_WROTE) {  // clear this lane's marks for the next batch
             smark[v] = 0xff;
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) *(((nbr >> i) & 1u) ? &nmark[cell[i]] : dum) = 0xff;
@@ -508,7 +518,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // ---- 4. lane-parallel bookkeeping of the committed draws [0, end) ------------------
         const bool done = lane < end;
         const bool is_acc = (st & ST_AC) != 0;
-        n_prop += (hit && done) ? 1u : 0u;
+        const bool proposed = (st & LF_HIT) && done;
+        n_prop += proposed ? 1u : 0u;
         n_acc += is_acc ? 1u : 0u;
         n_ic += (st & ST_IC) ? 1u : 0u;
         n_ip += (st & ST_IP) ? 1u : 0u;
@@ -611,13 +622,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 }
             }
             if (trace_on) {
-                const uint64_t PM = __ballot(hit && done);
+                const uint64_t PM = __ballot(proposed);
                 const uint64_t mine = ACCM & bits_below(lane + 1);
                 const int src = mine ? 63 - __builtin_clzll(mine) : 0;
                 const int c_j = __shfl(cut_after, src), n_j = __shfl(nb_after, src);
                 const long long w_j = __shfl((long long)my_wait, src);
                 const int64_t idx = trace_len + __popcll(PM & bits_below(lane));
-                if (hit && done && idx < p.trace_cap) {
+                if (proposed && idx < p.trace_cap) {
                     fc_record &rr = p.trace[(size_t)c * p.trace_cap + idx];
                     const bool valid = (st & ST_VS) != 0;
                     rr.draw = (int64_t)d;
@@ -651,8 +662,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
 #ifdef FC_PHASE_PROF
+    wave_sync();
     if (p.prof && lane == 0)
-        for (int i = 0; i < kProfSlots; ++i) p.prof[(size_t)c * kProfSlots + i] = prof_acc[i];
+        for (int i = 0; i < kProfSlots; ++i) p.prof[(size_t)c * kProfSlots + i] = prof_acc[i];  // after wave_sync
 #endif
 
     // ---- write back ---------------------------------------------------------------------

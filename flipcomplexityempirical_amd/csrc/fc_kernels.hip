@@ -89,7 +89,8 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
     uint32_t n_prop = 0, n_acc = 0, n_ic = 0, n_ip = 0;
 #ifdef FC_PHASE_PROF
-    int64_t prof_acc[kProfSlots] = {};
+    int64_t *prof_acc = (int64_t *)(base + p.chain_lds_bytes - kProfSlots * 8);
+    if (lane < kProfSlots) prof_acc[lane] = 0;
 #endif
     wave_sync();
     FC_STAMP(t_loop0);
@@ -574,8 +575,9 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
 #ifdef FC_PHASE_PROF
+    wave_sync();
     if (p.prof && lane == 0)
-        for (int i = 0; i < kProfSlots; ++i) p.prof[(size_t)c * kProfSlots + i] = prof_acc[i];
+        for (int i = 0; i < kProfSlots; ++i) p.prof[(size_t)c * kProfSlots + i] = prof_acc[i];  // after wave_sync
 #endif
 
     // ---- write back ---------------------------------------------------------------------
