@@ -281,7 +281,7 @@ def main():
         "bfs_per_proposal": float((s1["bfs_calls"] - s0["bfs_calls"]).sum()) * world / props if props else None,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": f"flip_kernel<{fg.info['ring_max']}, 1, {2 if W.k == 2 else 0}>",
+                     "kernel": run.kernel_name(),
                      "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": alg_bytes,
                      "lds": {"peak": LDS_PEAK_GBS, "frac": achieved / LDS_PEAK_GBS}},

@@ -29,7 +29,7 @@ EXPORTED = [
     "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
     "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_trace_reset", "fc_run_read_hist",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
-    "fc_run_n_chains", "fc_run_destroy",
+    "fc_run_frame_series", "fc_run_kernel_name", "fc_run_n_chains", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
 ]
 
@@ -120,6 +120,9 @@ def load(build_if_missing: bool = True):
     L.fc_run_read_events.argtypes = [vp, i32, _P(Event), i64, _P(i64)]
     L.fc_run_series_reset.argtypes = [vp]
     L.fc_run_autocorr.argtypes = [vp, _P(i32), i32, _P(i64), _P(dbl)]
+    L.fc_run_frame_series.argtypes = [vp, i32, i32, i32, _P(i32), _P(i32), _P(dbl), dbl, dbl, i64, _P(dbl),
+                                      _P(dbl), _P(i32), _P(i64)]
+    L.fc_run_kernel_name.argtypes = [vp, ctypes.c_char_p, i32]
     L.fc_run_n_chains.argtypes = [vp]
     L.fc_run_n_chains.restype = i32
     L.fc_run_destroy.argtypes = [vp]

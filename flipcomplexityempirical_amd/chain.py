@@ -39,7 +39,7 @@ from typing import Any, Callable, Dict, Hashable, Iterable, List, Optional, Sequ
 import numpy as np
 
 from . import _lib
-from .graphs import GraphSpec, from_networkx, log1mp_table
+from .graphs import GraphSpec, from_networkx, log1mp_table, slope_frame
 
 # ----------------------------------------------------------------------------------------
 # gerrychain updaters / constraints restated for host-side use  [gc-0.2]
@@ -387,14 +387,14 @@ class MarkovChain:
     def __len__(self):
         return self.total_steps
 
-    def _make_run(self, trace: bool, diag: int):
+    def _make_run(self, trace: bool, diag: int, event_cap: int = 0):
         from .engine import FlipGraph, FlipRun, RunConfig
         if self._graph is None:
             self._graph = FlipGraph(self.cspec.spec)
         cfg = RunConfig(seed=self.seed, chain_id_offset=self.chain_id, pop_lo=self.cspec.pop_lo,
                         pop_hi=self.cspec.pop_hi, base=self.cspec.base, device=self.device, diag_mask=diag,
                         trace_chains=1 if trace else 0, trace_cap=64 * self.chunk + 4096 if trace else 0,
-                        labels=tuple(self.cspec.labels))
+                        labels=tuple(self.cspec.labels), event_cap=event_cap)
         return FlipRun(self._graph, self.cspec.init[None, :], cfg)
 
     # ---- per-step iteration (debugging path) -------------------------------------------
@@ -423,14 +423,33 @@ class MarkovChain:
         run.close()
 
     # ---- fast path -------------------------------------------------------------------
-    def run(self) -> "ChainResult":
+    def run(self, series: bool = True, frame: Optional[str] = "auto") -> "ChainResult":
         """All ``total_steps`` yields on the device; the reference driver's outputs
-        (``grid_chain_sec11.py:366-419``) come back as a :class:`ChainResult`."""
+        (``grid_chain_sec11.py:366-419``) come back as a :class:`ChainResult`.
+
+        ``series`` keeps the per-yield lists ``rce`` / ``rbn`` (``:367-369``) through the
+        device event log; ``frame`` ("sec11", "frank", None or "auto": from the
+        ``slope`` updater and the node labels) adds the ``slopes`` / ``angles`` lists
+        (``:371-394``) computed by ``fc_run_frame_series``."""
         diag = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
-        run = self._make_run(trace=False, diag=diag)
+        if frame == "auto":
+            frame = None
+            if series and _name(self.initial_state.updaters.get("slope")) == "boundary_slope":
+                neg = any(isinstance(nd, tuple) and nd[1] < 0 for nd in self.cspec.spec.nodes)
+                frame = "frank" if neg else "sec11"
+        if series:
+            diag |= _lib.FC_DIAG_SERIES
+        run = self._make_run(trace=False, diag=diag, event_cap=max(self.total_steps, 1) if series else 0)
         if self.total_steps > 1:
             run.steps(self.total_steps - 1)
         res = ChainResult.from_run(self, run, 0)
+        if series:
+            res.rce = run.yield_values("cut", 0)
+            res.rbn = run.yield_values("nb", 0)
+            if frame is not None:
+                fs = run.frame_series(slope_frame(self.cspec.spec, frame), chains=[0])
+                res.slopes = run.yield_series(fs["slope"][0], 0)
+                res.angles = run.yield_series(fs["angle"][0], 0)
         run.close()
         return res
 
@@ -454,6 +473,47 @@ class ChainResult:
     lognum_flips: Dict[Hashable, float]
     final_assignment: Dict[Hashable, Any]
     stats: Dict[str, int] = field(default_factory=dict)
+    rce: Optional[np.ndarray] = None     # per-yield len(cut_edges)   (:367)
+    rbn: Optional[np.ndarray] = None     # per-yield len(b_nodes)     (:369)
+    slopes: Optional[np.ndarray] = None  # per-yield slope            (:371-382)
+    angles: Optional[np.ndarray] = None  # per-yield angle            (:389-394)
+
+    def heatmaps(self, shape=(40, 40), offset=(0, 0)) -> Dict[str, np.ndarray]:
+        """The driver's ``A2`` arrays (``grid_chain_sec11.py:431-528``): ``A2[n[0], n[1]]``
+        (FRANK: ``shape=(20, 40), offset=(0, 19)``, ``Frankenstein_chain.py:468-549``) of the
+        final assignment (``end2``), ``part_sum`` (``wca2``), ``num_flips`` (``flip2``) and
+        ``lognum_flips`` (``logflip2``)."""
+        out = {}
+        for name, vals in (("end2", self.final_assignment), ("wca2", self.part_sum),
+                           ("flip2", self.num_flips), ("logflip2", self.lognum_flips)):
+            A2 = np.zeros(shape)
+            for n, x in vals.items():
+                A2[n[0] + offset[0], n[1] + offset[1]] = x
+            out[name] = A2
+        return out
+
+    def write_outputs(self, directory: str, prefix: str, shape=(40, 40), offset=(0, 0)) -> List[str]:
+        """Write what the reference's sweep leaves per configuration, as data: ``wait.txt``
+        (``str(sum(waits))``, ``:410-411``), the heatmap arrays, per-edge ``cut_times`` and
+        the per-yield series, as ``.npy`` beside it (the PNG plotting is out of scope).
+        ``prefix`` is the reference's ``f"{alignment}B{int(100*base)}P{int(100*pop1)}"``."""
+        import os
+        os.makedirs(directory, exist_ok=True)
+        paths = []
+        p = os.path.join(directory, prefix + "wait.txt")
+        with open(p, "w") as f:
+            f.write(str(self.waits_sum))
+        paths.append(p)
+        arrays = dict(self.heatmaps(shape, offset))
+        arrays["edges"] = np.asarray(list(self.cut_times.values()), dtype=np.int64)
+        for name in ("rce", "rbn", "slopes", "angles"):
+            if getattr(self, name) is not None:
+                arrays[name] = getattr(self, name)
+        for name, arr in arrays.items():
+            p = os.path.join(directory, prefix + name + ".npy")
+            np.save(p, arr)
+            paths.append(p)
+        return paths
 
     @classmethod
     def from_run(cls, chain: MarkovChain, run, c: int) -> "ChainResult":

@@ -53,6 +53,8 @@ struct fc_run {
     uint32_t *d_tape = nullptr;
     int64_t tape_draws = 0;
     int64_t *d_prof = nullptr;  // FC_PHASE_PROF builds
+    int8_t *d_ser_a0 = nullptr;  // FC_DIAG_SERIES: assignment at the series window start
+    char kname[96] = {0};        // last launched flip-kernel instance
 };
 
 namespace {
@@ -83,7 +85,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc, r->d_edge_since,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events, r->d_prof};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events, r->d_prof, r->d_ser_a0};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -386,6 +388,8 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         if (E > 65535) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: FC_DIAG_SERIES stores |cut| in 16 bits (E <= 65535)");
         r->ev_cap = p->event_cap;
         if ((rc = dalloc(&r->d_events, (size_t)n_chains * (size_t)p->event_cap))) return rc;
+        if ((rc = dalloc(&r->d_ser_a0, assign.size()))) return rc;
+        HIP_TRY(hipMemcpy(r->d_ser_a0, r->d_assign, assign.size(), hipMemcpyDeviceToDevice));
     } else {
         r->p.diag_mask &= ~FC_DIAG_SERIES;
     }
@@ -492,7 +496,8 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     for (int64_t done = 0; done < n_steps; done += kChunk) {
         k.n_steps = std::min(kChunk, n_steps - done);
         if (max_draws <= 0) k.max_draws = 65536 * k.n_steps;
-        const int e = r->p.k == 2 ? fc::launch_flip2(k, r->g.ring_max, s) : fc::launch_flip_k2(k, r->g.ring_max, s);
+        const int e = r->p.k == 2 ? fc::launch_flip2(k, r->g.ring_max, s, r->kname, sizeof r->kname)
+                                    : fc::launch_flip_k2(k, r->g.ring_max, s, r->kname, sizeof r->kname);
         if (e != 0) return fail(FC_ERR_HIP, std::string("flip kernel launch: ") + hipGetErrorString((hipError_t)e));
     }
     HIP_TRY(hipEventRecord(evp.second, s));
@@ -659,6 +664,8 @@ int fc_run_series_reset(fc_run *r) {
         s.ser_nb0 = s.nb;
     }
     HIP_TRY(hipMemcpy(r->d_sc, sc.data(), sc.size() * sizeof(sc[0]), hipMemcpyHostToDevice));
+    if (r->d_ser_a0)
+        HIP_TRY(hipMemcpy(r->d_ser_a0, r->d_assign, (size_t)r->n_chains * r->npad, hipMemcpyDeviceToDevice));
     return FC_OK;
 }
 
@@ -748,6 +755,94 @@ int fc_run_autocorr(fc_run *r, const int32_t *lags, int32_t nlags, int64_t *lag_
     const int rc = run();
     cleanup();
     return rc;
+}
+
+int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *frame_u,
+                        const int32_t *frame_v, const double *mid_xy, double cx, double cy, int64_t cap,
+                        double *slope, double *angle, int32_t *n_cut, int64_t *len) {
+    if (!r || !frame_u || !frame_v || !mid_xy || !slope || !angle || !n_cut || !len)
+        return fail(FC_ERR_ARG, "fc_run_frame_series: null argument");
+    if (!r->d_events) return fail(FC_ERR_ARG, "fc_run_frame_series: FC_DIAG_SERIES not enabled");
+    if (r->p.k != 2)
+        return fail(FC_ERR_UNSUPPORTED, "fc_run_frame_series: the frame series follows k = 2 flips (the reference "
+                                        "computes boundary_slope only in its two-district drivers)");
+    if (c0 < 0 || nc < 0 || c0 + nc > r->n_chains) return fail(FC_ERR_ARG, "fc_run_frame_series: chain range");
+    if (n_frame < 0 || n_frame > 256) return fail(FC_ERR_UNSUPPORTED, "fc_run_frame_series: at most 256 frame edges");
+    const int32_t n = r->g.n;
+    std::vector<int32_t> tog_idx(n, -1);
+    std::vector<uint64_t> tog;
+    for (int32_t j = 0; j < n_frame; ++j) {
+        const int32_t ends[2] = {frame_u[j], frame_v[j]};
+        if (ends[0] < 0 || ends[0] >= n || ends[1] < 0 || ends[1] >= n || ends[0] == ends[1])
+            return fail(FC_ERR_ARG, "fc_run_frame_series: frame edge " + std::to_string(j) + " out of range");
+        for (int32_t x : ends) {
+            if (tog_idx[x] < 0) {
+                tog_idx[x] = (int32_t)(tog.size() / 4);
+                tog.insert(tog.end(), 4, 0);
+            }
+            tog[(size_t)tog_idx[x] * 4 + (j >> 6)] |= uint64_t(1) << (j & 63);
+        }
+    }
+    if (nc == 0) return FC_OK;
+    if (int rc = fc_run_sync(r)) return rc;
+    std::vector<fc::ChainScalars> sc(nc);
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc + c0, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    std::vector<int64_t> ev_len(r->n_chains, 0);
+    for (int32_t i = 0; i < nc; ++i) {
+        if (sc[i].ev_len > r->ev_cap)
+            return fail(FC_ERR_ARG, "fc_run_frame_series: chain " + std::to_string(c0 + i) +
+                                        " overflowed event_cap; reset the series window more often");
+        if (sc[i].ev_len + 1 > cap)
+            return fail(FC_ERR_ARG, "fc_run_frame_series: cap < events + 1 for chain " + std::to_string(c0 + i));
+        ev_len[c0 + i] = sc[i].ev_len;
+        len[i] = sc[i].ev_len + 1;
+    }
+    int32_t *d_fuv = nullptr, *d_tidx = nullptr, *d_cnt = nullptr;
+    int64_t *d_len = nullptr;
+    uint64_t *d_tog = nullptr;
+    double *d_mid = nullptr, *d_out = nullptr;
+    auto cleanup = [&]() {
+        for (void *b : {(void *)d_fuv, (void *)d_tidx, (void *)d_cnt, (void *)d_len, (void *)d_tog, (void *)d_mid,
+                        (void *)d_out})
+            if (b) (void)hipFree(b);
+    };
+    auto run = [&]() -> int {
+        int q;
+        const size_t outn = (size_t)nc * cap;
+        if ((q = dalloc(&d_fuv, (size_t)2 * std::max(n_frame, 1)))) return q;
+        if ((q = dalloc(&d_tidx, (size_t)n))) return q;
+        if ((q = dalloc(&d_tog, std::max<size_t>(tog.size(), 4)))) return q;
+        if ((q = dalloc(&d_mid, (size_t)2 * std::max(n_frame, 1)))) return q;
+        if ((q = dalloc(&d_len, (size_t)r->n_chains))) return q;
+        if ((q = dalloc(&d_out, 2 * outn))) return q;
+        if ((q = dalloc(&d_cnt, outn))) return q;
+        if (n_frame) {
+            HIP_TRY(hipMemcpy(d_fuv, frame_u, (size_t)n_frame * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(d_fuv + n_frame, frame_v, (size_t)n_frame * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(d_mid, mid_xy, (size_t)n_frame * 16, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(d_tog, tog.data(), tog.size() * 8, hipMemcpyHostToDevice));
+        }
+        HIP_TRY(hipMemcpy(d_tidx, tog_idx.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_len, ev_len.data(), ev_len.size() * 8, hipMemcpyHostToDevice));
+        int e = fc::launch_frame_series(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, d_len, c0, nc, n_frame, d_fuv,
+                                        d_fuv + n_frame, d_mid, cx, cy, d_tidx, d_tog, cap, d_out, d_out + outn,
+                                        d_cnt, r->stream);
+        if (e) return fail(FC_ERR_HIP, std::string("frame series: ") + hipGetErrorString((hipError_t)e));
+        HIP_TRY(hipStreamSynchronize(r->stream));
+        HIP_TRY(hipMemcpy(slope, d_out, outn * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(angle, d_out + outn, outn * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(n_cut, d_cnt, outn * 4, hipMemcpyDeviceToHost));
+        return FC_OK;
+    };
+    const int rc = run();
+    cleanup();
+    return rc;
+}
+
+int fc_run_kernel_name(const fc_run *r, char *buf, int32_t cap) {
+    if (!r || !buf || cap <= 0) return fail(FC_ERR_ARG, "fc_run_kernel_name: null argument");
+    std::snprintf(buf, (size_t)cap, "%s", r->kname);
+    return FC_OK;
 }
 
 int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist) {

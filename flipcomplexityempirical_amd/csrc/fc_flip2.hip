@@ -23,6 +23,8 @@
 //   4. the per-yield diagnostics are accumulated lane-parallel from per-slot status bits.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "fc_device.h"
 #include "fc_internal.h"
 #include "fc_philox.h"
@@ -720,7 +722,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     }
 }
 
-int launch_flip2(const KParams &p, int ring_max, void *stream) {
+int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap) {
     const int wpb = waves_per_block(p.chain_lds_bytes);
     const int blocks = (p.n_chains + wpb - 1) / wpb;
     const size_t lds = (size_t)p.chain_lds_bytes * wpb;
@@ -734,6 +736,7 @@ int launch_flip2(const KParams &p, int ring_max, void *stream) {
         if (lds > 65536)                                                                                \
             (void)hipFuncSetAttribute((const void *)flip2_kernel<R, S, F>,                              \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
+        if (name) snprintf(name, name_cap, "fc::flip2_kernel<%d, %d, %s>", R, S, F ? "true" : "false"); \
         hipLaunchKernelGGL((flip2_kernel<R, S, F>), grid, block, lds, s, p);                            \
     } while (0)
 #define FC_FULL2(R, S)                   \

@@ -124,8 +124,9 @@ struct KParams {
 constexpr int kProfSlots = 16;
 
 // Launch wrappers (fc_kernels.hip).  Return a hipError_t as int.
-int launch_flip_k2(const KParams &p, int ring_max, void *stream);   // k > 2 (fc_kernels.hip)
-int launch_flip2(const KParams &p, int ring_max, void *stream);     // k = 2 (fc_flip2.hip)
+// `name` (may be null) receives the launched instance, spelled as rocprofv3 reports it.
+int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap);  // k > 2
+int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap);    // k = 2
 int launch_init_fcnt(const KParams &p, int ring_max, void *stream);
 
 // Series diagnostics (fc_series.hip): expand the event logs of chains [c0, c0 + nc) into
@@ -137,5 +138,13 @@ int launch_series_expand(const fc_event *events, int64_t ev_cap, const int64_t *
 int launch_series_lagsums(const uint16_t *x, const int64_t *len, int32_t c0, int32_t nc, int64_t stride,
                           int64_t max_len, const int32_t *lags, int32_t nlags, unsigned long long *sums,
                           void *stream);
+// Frame-edge slope / angle series of chains [c0, c0 + nc), k = 2 (fc_series.hip): entry 0 is
+// the window start (assignment a0), entry i + 1 the state after event i.  tog_idx[node] is the
+// node's row in tog_mask[.][4] (frame edges incident to it) or -1.  n_frame <= 256.
+int launch_frame_series(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
+                        const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
+                        const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
+                        const uint64_t *tog_mask, int64_t cap, double *slope, double *angle, int32_t *cnt,
+                        void *stream);
 
 }  // namespace fc

@@ -23,6 +23,8 @@
 //       lane-parallel from the per-lane status bits.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "fc_internal.h"
 #include "fc_philox.h"
 #include "fc_device.h"
@@ -632,7 +634,7 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     }
 }
 
-int launch_flip_k2(const KParams &p, int ring_max, void *stream) {
+int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap) {
     const int wpb = waves_per_block(p.chain_lds_bytes);
     const int blocks = (p.n_chains + wpb - 1) / wpb;
     const size_t lds = (size_t)p.chain_lds_bytes * wpb;
@@ -647,6 +649,7 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream) {
         if (lds > 65536)                                                                                \
             (void)hipFuncSetAttribute((const void *)flip_kernel<R, S, K, F>,                            \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
+        if (name) snprintf(name, name_cap, "fc::flip_kernel<%d, %d, %d, %s>", R, S, K, F ? "true" : "false"); \
         hipLaunchKernelGGL((flip_kernel<R, S, K, F>), grid, block, lds, s, p);                          \
     } while (0)
 #define FC_FULL_SWITCH(R, S, K)                          \

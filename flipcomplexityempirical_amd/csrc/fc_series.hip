@@ -96,6 +96,116 @@ __global__ __launch_bounds__(kThreads) void series_lagsum_kernel(const uint16_t 
     }
 }
 
+// ---- frame-edge slope / angle series (boundary_slope + the driver's loop body,
+// grid_chain_sec11.py:55-78,371-394; Frankenstein_chain.py:55-78,399-422), k = 2.
+//
+// One wavefront per chain.  Only frame edges matter, and for k = 2 an event at node v
+// toggles the cut status of exactly the frame edges incident to v, so the frame-cut mask
+// after event i is mask0 ^ (prefix-XOR of the toggle masks of events 0..i): each lane
+// takes one event of a 64-event chunk and a wave XOR scan gives every lane its state.
+constexpr int kFrameWords = 4;  // up to 256 frame edges
+
+__device__ inline uint64_t shfl_up64(uint64_t x, int off) {
+    return (uint64_t)__shfl_up((long long)x, off);
+}
+
+// slope and angle from the first two frame cut edges (canonical order); NaN with < 2
+__device__ inline void frame_eval(const uint64_t m[kFrameWords], const double *__restrict__ mid, double cx,
+                                  double cy, double &slope, double &angle, int &cnt) {
+#pragma clang fp contract(off)
+    int j0 = -1, j1 = -1;
+    cnt = 0;
+#pragma unroll
+    for (int w = 0; w < kFrameWords; ++w) {
+        uint64_t x = m[w];
+        cnt += __popcll(x);
+        if (j1 < 0 && x) {
+            if (j0 < 0) {
+                j0 = 64 * w + __builtin_ctzll(x);
+                x &= x - 1;
+            }
+            if (x) j1 = 64 * w + __builtin_ctzll(x);
+        }
+    }
+    if (cnt < 2) {  // the reference raises IndexError on temp[1] here
+        slope = __builtin_nan("");
+        angle = __builtin_nan("");
+        return;
+    }
+    const double ax = mid[2 * j0], ay = mid[2 * j0 + 1], bx = mid[2 * j1], by = mid[2 * j1 + 1];
+    // slope = (endb[1]-enda[1])/(endb[0]-enda[0]) else np.Inf  (:378-382)
+    slope = (bx != ax) ? (by - ay) / (bx - ax) : __builtin_inf();
+    // arccos(clip(dot(a/|a|, b/|b|), -1, 1)) about (20, 20)  (:389-394)
+    const double pax = ax - cx, pay = ay - cy, pbx = bx - cx, pby = by - cy;
+    const double na = sqrt(pax * pax + pay * pay), nb = sqrt(pbx * pbx + pby * pby);
+    double d = (pax / na) * (pbx / nb) + (pay / na) * (pby / nb);
+    d = d < -1.0 ? -1.0 : (d > 1.0 ? 1.0 : d);
+    angle = acos(d);
+}
+
+__global__ __launch_bounds__(kThreads) void frame_series_kernel(
+    const int8_t *__restrict__ a0, int32_t npad, const fc_event *__restrict__ events, int64_t ev_cap,
+    const int64_t *__restrict__ ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *__restrict__ fu,
+    const int32_t *__restrict__ fv, const double *__restrict__ mid, double cx, double cy,
+    const int32_t *__restrict__ tog_idx, const uint64_t *__restrict__ tog_mask, int64_t cap,
+    double *__restrict__ slope_out, double *__restrict__ angle_out, int32_t *__restrict__ cnt_out) {
+    const int lane = threadIdx.x & 63;
+    const int32_t cl = (int32_t)(blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
+    if (cl >= nc) return;  // whole wave
+    const int32_t c = c0 + cl;
+    const int8_t *a = a0 + (size_t)c * npad;
+    uint64_t m[kFrameWords];
+#pragma unroll
+    for (int w = 0; w < kFrameWords; ++w) {
+        const int j = 64 * w + lane;
+        const bool cut = j < n_frame && a[fu[j]] != a[fv[j]];
+        m[w] = __ballot(cut);
+    }
+    double *so = slope_out + (size_t)cl * cap, *ao = angle_out + (size_t)cl * cap;
+    int32_t *co = cnt_out + (size_t)cl * cap;
+    if (lane == 0) {
+        double sl, an;
+        int cnt;
+        frame_eval(m, mid, cx, cy, sl, an, cnt);
+        so[0] = sl;
+        ao[0] = an;
+        co[0] = cnt;
+    }
+    const fc_event *ev = events + (size_t)c * ev_cap;
+    const int64_t ne = ev_len[c];
+    for (int64_t b = 0; b < ne; b += 64) {
+        const int64_t i = b + lane;
+        uint64_t t[kFrameWords] = {0, 0, 0, 0};
+        if (i < ne) {
+            const int32_t s = tog_idx[ev[i].v];
+            if (s >= 0) {
+#pragma unroll
+                for (int w = 0; w < kFrameWords; ++w) t[w] = tog_mask[(size_t)s * kFrameWords + w];
+            }
+        }
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+            for (int w = 0; w < kFrameWords; ++w) {
+                const uint64_t y = shfl_up64(t[w], off);
+                if (lane >= off) t[w] ^= y;
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < kFrameWords; ++w) t[w] ^= m[w];
+        if (i < ne) {
+            double sl, an;
+            int cnt;
+            frame_eval(t, mid, cx, cy, sl, an, cnt);
+            so[i + 1] = sl;
+            ao[i + 1] = an;
+            co[i + 1] = cnt;
+        }
+#pragma unroll
+        for (int w = 0; w < kFrameWords; ++w) m[w] = (uint64_t)__shfl((long long)t[w], 63);
+    }
+}
+
 }  // namespace
 
 int launch_series_expand(const fc_event *events, int64_t ev_cap, const int64_t *ev_len, const int64_t *t0,
@@ -115,6 +225,24 @@ int launch_series_lagsums(const uint16_t *x, const int64_t *len, int32_t c0, int
     const dim3 grid((unsigned)((max_len + kTile - 1) / kTile), (unsigned)nc);
     hipLaunchKernelGGL(series_lagsum_kernel, grid, dim3(kThreads), 0, (hipStream_t)stream, x, len, c0, stride, lags,
                        nlags, sums);
+    return (int)hipGetLastError();
+}
+
+}  // namespace fc
+
+namespace fc {
+
+int launch_frame_series(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
+                        const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
+                        const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
+                        const uint64_t *tog_mask, int64_t cap, double *slope, double *angle, int32_t *cnt,
+                        void *stream) {
+    if (nc <= 0) return (int)hipSuccess;
+    if (n_frame > 64 * kFrameWords) return (int)hipErrorInvalidValue;
+    const int wpb = kThreads / 64;
+    const dim3 grid((unsigned)((nc + wpb - 1) / wpb));
+    hipLaunchKernelGGL(frame_series_kernel, grid, dim3(kThreads), 0, (hipStream_t)stream, a0, npad, events, ev_cap,
+                       ev_len, c0, nc, n_frame, fu, fv, mid, cx, cy, tog_idx, tog_mask, cap, slope, angle, cnt);
     return (int)hipGetLastError();
 }
 

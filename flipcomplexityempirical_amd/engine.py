@@ -251,6 +251,14 @@ class FlipRun:
         vals = np.concatenate([[x0], ev["cut"].astype(np.int64)])
         return np.repeat(vals, np.diff(bounds))
 
+    def yield_values(self, field: str = "cut", chain: int = 0) -> np.ndarray:
+        """Per-yield ``|cut|`` ("cut") or ``|B|`` ("nb") over the window: the reference's
+        ``rce`` / ``rbn`` lists (``grid_chain_sec11.py:367,369``)."""
+        st = self.stats()
+        x0 = int(st["series_cut0" if field == "cut" else "series_nb0"][chain])
+        ev = self.events(chain)
+        return self.yield_series(np.concatenate([[x0], ev[field].astype(np.int64)]), chain)
+
     def autocorr(self, lags: Sequence[int]):
         """Device autocorrelation of the |cut| series over the window: ``(lag_sums, acf)``,
         each ``[n_chains, len(lags)]`` (``fc_run_autocorr``)."""
@@ -260,6 +268,51 @@ class FlipRun:
         check(_lib.load().fc_run_autocorr(self.handle, _p(lg, ctypes.c_int32), int(lg.size),
                                           _p(sums, ctypes.c_int64), _p(acf, ctypes.c_double)), "fc_run_autocorr")
         return sums, acf
+
+    def frame_series(self, frame, chains: Optional[Sequence[int]] = None) -> Dict[str, np.ndarray]:
+        """Slope / angle of the frame cut edges after every accepted flip of the window, on
+        the device (``fc_run_frame_series``; ``grid_chain_sec11.py:55-78,371-394``).
+
+        ``frame`` is a :class:`~flipcomplexityempirical_amd.graphs.SlopeFrame`.  Returns
+        ``slope``, ``angle``, ``n_cut`` as ``[len(chains), max_events + 1]`` (entry 0: window
+        start) and ``len`` per chain; use :meth:`yield_series` for the per-yield lists."""
+        ch = np.arange(self.n_chains) if chains is None else np.asarray(chains, dtype=np.int64)
+        if ch.size == 0:
+            raise ValueError("frame_series: no chains")
+        c0, nc = int(ch.min()), int(ch.max() - ch.min() + 1)
+        st = self.stats()
+        cap = int(st["events"][c0:c0 + nc].max()) + 1
+        slope = np.zeros((nc, cap), dtype=np.float64)
+        angle = np.zeros((nc, cap), dtype=np.float64)
+        ncut = np.zeros((nc, cap), dtype=np.int32)
+        ln = np.zeros(nc, dtype=np.int64)
+        eu = np.ascontiguousarray(frame.eu, dtype=np.int32)
+        ev = np.ascontiguousarray(frame.ev, dtype=np.int32)
+        mid = np.ascontiguousarray(frame.mid, dtype=np.float64)
+        check(_lib.load().fc_run_frame_series(self.handle, c0, nc, int(eu.size), _p(eu, ctypes.c_int32),
+                                              _p(ev, ctypes.c_int32), _p(mid, ctypes.c_double),
+                                              float(frame.center[0]), float(frame.center[1]), cap,
+                                              _p(slope, ctypes.c_double), _p(angle, ctypes.c_double),
+                                              _p(ncut, ctypes.c_int32), _p(ln, ctypes.c_int64)),
+              "fc_run_frame_series")
+        sel = ch - c0
+        return {"slope": slope[sel], "angle": angle[sel], "n_cut": ncut[sel], "len": ln[sel]}
+
+    def yield_series(self, values: np.ndarray, chain: int = 0) -> np.ndarray:
+        """Expand a per-event series (entry 0 = window start, as ``frame_series`` returns it)
+        to one value per yield of the window, as the reference's ``slopes`` / ``angles``
+        lists hold them (``grid_chain_sec11.py:382,394``)."""
+        st = self.stats()
+        t0, T = int(st["series_t0"][chain]), int(st["steps"][chain])
+        ev = self.events(chain)
+        bounds = np.concatenate([[t0], ev["t"], [T + 1]]).astype(np.int64)
+        return np.repeat(np.asarray(values)[:ev.size + 1], np.diff(bounds))
+
+    def kernel_name(self) -> str:
+        """The flip-kernel instance the last ``steps`` call launched (rocprofv3 spelling)."""
+        buf = ctypes.create_string_buffer(128)
+        check(_lib.load().fc_run_kernel_name(self.handle, buf, 128), "fc_run_kernel_name")
+        return buf.value.decode()
 
     def close(self):
         if getattr(self, "handle", None):

@@ -288,6 +288,49 @@ def bisection_plan(spec: GraphSpec, k: int) -> Dict:
 
 
 # --------------------------------------------------------------------------------------
+# Frame edges for the slope / angle diagnostic (boundary_slope)
+# --------------------------------------------------------------------------------------
+# boundary_slope keeps the cut edges whose two endpoints share one frame coordinate, plus
+# (sec11 only) the four corner diagonals: grid_chain_sec11.py:55-78 (lines x=0, y=0,
+# x=39, y=39) and Frankenstein_chain.py:55-78 (x=0, y=-19, x=19, y=20, diagonals
+# commented out).  The angle is taken about (20, 20) in both drivers (:389-390, :417-418).
+FRAME_RULES = {
+    "sec11": {"lines": ((0, 0), (1, 0), (0, 39), (1, 39)), "diagonals": SEC11_DIAGONALS, "center": (20.0, 20.0)},
+    "frank": {"lines": ((0, 0), (1, -19), (0, 19), (1, 20)), "diagonals": (), "center": (20.0, 20.0)},
+}
+
+
+@dataclass
+class SlopeFrame:
+    """Frame edges (canonical-edge order), their midpoints and the angle centre."""
+
+    eu: np.ndarray    # int32 [F]
+    ev: np.ndarray    # int32 [F]
+    mid: np.ndarray   # float64 [F, 2]: ((u0+v0)/2, (u1+v1)/2) in node-label coordinates
+    center: tuple
+
+
+def slope_frame(spec: GraphSpec, kind: str = "sec11") -> SlopeFrame:
+    """The edges ``boundary_slope`` can ever return: its filter applied to every edge.
+
+    With both districts contiguous on a disc-like lattice exactly two frame edges are cut,
+    so the result does not depend on which two the reference's set order picks first; for
+    more, the device uses the first two in this (canonical edge) order."""
+    rule = FRAME_RULES[kind]
+    diag = {tuple(d) for d in rule["diagonals"]} | {(d[1], d[0]) for d in rule["diagonals"]}
+    eu, ev, mid = [], [], []
+    for u, v in spec.edges():
+        a, b = spec.nodes[int(u)], spec.nodes[int(v)]
+        on_line = any(a[axis] == val and b[axis] == val for axis, val in rule["lines"])
+        if on_line or (a, b) in diag:
+            eu.append(int(u))
+            ev.append(int(v))
+            mid.append(((a[0] + b[0]) / 2, (a[1] + b[1]) / 2))
+    return SlopeFrame(eu=np.asarray(eu, dtype=np.int32), ev=np.asarray(ev, dtype=np.int32),
+                      mid=np.asarray(mid, dtype=np.float64).reshape(-1, 2), center=rule["center"])
+
+
+# --------------------------------------------------------------------------------------
 # Known answers used by tests (host-side, networkx)
 # --------------------------------------------------------------------------------------
 def cut_and_boundary(spec: GraphSpec, assign: np.ndarray):

@@ -196,6 +196,23 @@ int fc_run_series_reset(fc_run *r);
  * mean (the biased sample ACF, statsmodels' acf default), formed on the host from exact
  * integer sums.  FC_ERR_ARG if a chain's event log overflowed event_cap. */
 int fc_run_autocorr(fc_run *r, const int32_t *lags, int32_t nlags, int64_t *lag_sums, double *acf);
+/* Frame-edge slope / angle series of chains [c0, c0 + nc) over the current window
+ * (boundary_slope + the driver's loop body, grid_chain_sec11.py:55-78,371-394;
+ * Frankenstein_chain.py:55-78,399-422).  k = 2 only (FC_ERR_UNSUPPORTED otherwise).
+ *   frame_u/v [n_frame <= 256]: the frame edges boundary_slope can return, in the order
+ *                               whose first two cut members are used;
+ *   mid_xy [2 n_frame]:          their midpoints (enda / endb) in the reference's node
+ *                               coordinates; (cx, cy) the angle centre ((20, 20) there).
+ * Output [i * cap + j] for chain c0 + i: j = 0 the window start yield, j >= 1 the state
+ * created by event j - 1 (it holds for yields event.t .. next event.t - 1):
+ *   slope (+inf when the two midpoints share x), angle = arccos(clip(cos)), n_cut = frame
+ *   cut edges (< 2: slope = angle = NaN, where the reference raises IndexError).
+ * len[i] = events + 1.  FC_ERR_ARG when cap is too small or a log overflowed event_cap. */
+int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *frame_u,
+                        const int32_t *frame_v, const double *mid_xy, double cx, double cy, int64_t cap,
+                        double *slope, double *angle, int32_t *n_cut, int64_t *len);
+/* Name of the last launched flip-kernel instance, as rocprofv3 spells it. */
+int fc_run_kernel_name(const fc_run *r, char *buf, int32_t cap);
 int32_t fc_run_n_chains(const fc_run *r);
 void fc_run_destroy(fc_run *r);
 

@@ -512,3 +512,58 @@ def acf_float(x: np.ndarray, lags) -> np.ndarray:
     den = float(np.dot(d, d))
     return np.asarray([float(np.dot(d[:len(d) - L], d[L:])) / den if L < len(d) and den else 0.0
                        for L in lags])
+
+
+# --------------------------------------------------------------------------------------
+# boundary_slope + the driver's slope / angle lines (checker for fc_run_frame_series).
+# grid_chain_sec11.py:55-78 (sec11 frame) and Frankenstein_chain.py:55-78 (FRANK frame),
+# loop body grid_chain_sec11.py:371-394 / Frankenstein_chain.py:399-422.  Restated over
+# node-label tuples exactly as the reference's updater sees partition["cut_edges"].
+# --------------------------------------------------------------------------------------
+_SEC11_E = [((0, 1), (1, 0)), ((0, 38), (1, 39)), ((38, 0), (39, 1)), ((38, 39), (39, 38))]
+_SEC11_E_REV = [((1, 0), (0, 1)), ((1, 39), (0, 38)), ((39, 1), (38, 0)), ((39, 38), (38, 39))]
+
+
+def boundary_slope(cut_edges, kind: str = "sec11") -> list:
+    """``boundary_slope(partition)`` on a cut-edge collection of node-label pairs."""
+    a, b, c, d, e = [], [], [], [], []
+    if kind == "sec11":
+        lim = (0, 0, 39, 39)
+    else:  # Frankenstein_chain.py:59-66
+        lim = (0, -19, 19, 20)
+    for x in cut_edges:
+        if x[0][0] == lim[0] and x[1][0] == lim[0]:
+            a.append(x)
+        elif x[0][1] == lim[1] and x[1][1] == lim[1]:
+            b.append(x)
+        elif x[0][0] == lim[2] and x[1][0] == lim[2]:
+            c.append(x)
+        elif x[0][1] == lim[3] and x[1][1] == lim[3]:
+            d.append(x)
+        elif kind == "sec11" and x in _SEC11_E:
+            e.append(x)
+        elif kind == "sec11" and x in _SEC11_E_REV:
+            e.append(x)
+    return list(set(a + b + c + d + e))
+
+
+def slope_angle(temp) -> tuple:
+    """The driver's per-yield lines on ``temp = part["slope"]`` (``:374-394``): raises
+    IndexError for fewer than two frame edges, as the reference does."""
+    enda = ((temp[0][0][0] + temp[0][1][0]) / 2, (temp[0][0][1] + temp[0][1][1]) / 2)
+    endb = ((temp[1][0][0] + temp[1][1][0]) / 2, (temp[1][0][1] + temp[1][1][1]) / 2)
+    if endb[0] != enda[0]:
+        slope = (endb[1] - enda[1]) / (endb[0] - enda[0])
+    else:
+        slope = np.inf
+    anga = (enda[0] - 20, enda[1] - 20)
+    angb = (endb[0] - 20, endb[1] - 20)
+    angle = np.arccos(np.clip(np.dot(anga / np.linalg.norm(anga), angb / np.linalg.norm(angb)), -1, 1))
+    return float(slope), float(angle)
+
+
+def cut_edge_labels(spec, assign: np.ndarray) -> set:
+    """gerrychain ``cut_edges`` of a district-id array, as sorted node-label tuples [gc-0.2]."""
+    e = spec.edges()
+    m = assign[e[:, 0]] != assign[e[:, 1]]
+    return {tuple(sorted((spec.nodes[u], spec.nodes[v]))) for u, v in e[m]}

@@ -1,0 +1,116 @@
+"""GPU parity of the frame slope / angle series.
+
+The reference computes, for every yielded state, ``temp = part["slope"]``
+(``boundary_slope``, ``grid_chain_sec11.py:55-78``; FRANK ``Frankenstein_chain.py:55-78``)
+and from its first two frame cut edges the slope of the chord and the angle it subtends
+about (20, 20) (``:371-394``).  The device derives both from the FC_DIAG_SERIES event log
+(``fc_run_frame_series``).  The checker replays the same events on the host, builds each
+state's ``cut_edges`` as node-label tuples and runs the oracle's restatement of
+``boundary_slope`` and of the loop body (numpy ``dot`` / ``linalg.norm`` / ``arccos``).
+
+Tolerances: the frame cut count is exact; the slope is exact (midpoints are halves, one
+subtraction each, one correctly rounded division; compared with ``==``, so -0.0 == 0.0:
+the sign of a zero slope follows the order of the two edges in the reference's set);
+the angle is within 1e-6 absolute -- a 1-ulp difference in the cosine (numpy/BLAS versus
+device summation order) is amplified by arccos near +-1 to ~3e-8.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from flipcomplexityempirical_amd import graphs as G
+from flipcomplexityempirical_amd import _lib
+from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+from oracle.flipref import boundary_slope, cut_edge_labels, slope_angle
+
+pytestmark = pytest.mark.gpu
+
+ANGLE_TOL = 1e-6
+
+
+def _run(spec, plans, bases, pct, seed=5):
+    fg = FlipGraph(spec)
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), 2, pct)
+    inits = np.stack([spec.assignment_array(p, [-1, 1]) for p in plans])
+    cfg = RunConfig(seed=seed, pop_lo=lo, pop_hi=hi, diag_mask=_lib.FC_DIAG_WAIT | _lib.FC_DIAG_SERIES,
+                    event_cap=100000)
+    return FlipRun(fg, inits, cfg, bases=np.asarray(bases, dtype=np.float64)), inits
+
+
+def _check_window(spec, kind, frame, run, c, a_start, out, i):
+    """Replay chain c's events from a_start; compare every state. Returns the end state."""
+    ev = run.events(c)
+    n = int(out["len"][i])
+    assert n == ev.size + 1
+    a = a_start.copy()
+    for j in range(n):
+        if j:
+            v = int(ev[j - 1]["v"])
+            assert a[v] != ev[j - 1]["target"]
+            a[v] = ev[j - 1]["target"]
+        temp = boundary_slope(cut_edge_labels(spec, a), kind)
+        assert int(out["n_cut"][i, j]) == len(temp), (c, j)
+        if len(temp) < 2:
+            with pytest.raises(IndexError):
+                slope_angle(temp)
+            assert math.isnan(out["slope"][i, j]) and math.isnan(out["angle"][i, j])
+            continue
+        s_ref, a_ref = slope_angle(temp)
+        assert out["slope"][i, j] == s_ref, (c, j, out["slope"][i, j], s_ref)
+        assert abs(out["angle"][i, j] - a_ref) <= ANGLE_TOL, (c, j, out["angle"][i, j], a_ref)
+    return a
+
+
+@pytest.mark.parametrize("kind", ["sec11", "frank"])
+def test_frame_series_matches_reference_loop_body(gpu, kind):
+    if kind == "sec11":
+        spec = G.sec11_graph()
+        plans = [G.sec11_plan(al, spec.nodes) for al in (0, 1, 2, 0, 1, 2)]
+        bases = [0.1, 0.38, 1.0, 2.63815853, 10.0, 1.0]
+    else:
+        spec = G.frank_graph()
+        plans = [G.frank_plan(al, spec.nodes) for al in (0, 1, 2, 0)]
+        bases = [0.3, 1 / 0.3, 1.0, 0.3]
+    frame = G.slope_frame(spec, kind)
+    run, inits = _run(spec, plans, bases, 0.5)
+    run.steps(1500)
+    out = run.frame_series(frame)
+    ends = [_check_window(spec, kind, frame, run, c, inits[c], out, c) for c in range(len(bases))]
+    fin = run.state()
+    for c in range(len(bases)):
+        assert np.array_equal(ends[c], fin[c])
+        ys = run.yield_series(out["slope"][c], c)
+        assert ys.size == 1500 + 1
+    # second window: starts from the state at the reset, on a chain subset
+    run.series_reset()
+    run.steps(1000)
+    out2 = run.frame_series(frame, chains=[1, 2, 3])
+    fin2 = run.state()
+    for i, c in enumerate([1, 2, 3]):
+        end = _check_window(spec, kind, frame, run, c, fin[c], out2, i)
+        assert np.array_equal(end, fin2[c])
+        assert run.yield_series(out2["angle"][i], c).size == 1000 + 1
+
+
+def test_frame_series_rejects_k_gt_2(gpu):
+    spec = G.sec11_graph()
+    fg = FlipGraph(spec)
+    a0 = spec.assignment_array(G.quadrant_plan(spec.nodes), list(range(4)))
+    _, (lo, hi) = G.population_bounds(spec.n, 4, 0.5)
+    run = FlipRun(fg, a0[None, :], RunConfig(k=4, labels=(0, 1, 2, 3), proposal=_lib.FC_PROPOSE_PAIR, seed=1,
+                                             pop_lo=lo, pop_hi=hi, diag_mask=_lib.FC_DIAG_SERIES,
+                                             event_cap=1000))
+    run.steps(10)
+    with pytest.raises(NotImplementedError):
+        run.frame_series(G.slope_frame(spec))
+
+
+def test_kernel_name_reported(gpu):
+    spec = G.sec11_graph()
+    fg = FlipGraph(spec)
+    a0 = spec.assignment_array(G.sec11_plan(0, spec.nodes), [-1, 1])
+    _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
+    run = FlipRun(fg, a0[None, :], RunConfig(seed=1, pop_lo=lo, pop_hi=hi))
+    run.steps(10)
+    assert run.kernel_name().startswith("fc::flip2_kernel<8, ")
