@@ -22,12 +22,13 @@ shutil.copy(os.path.join(src, f"prof_{tag}", "run_kernel_stats.csv"), os.path.jo
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     rows = [r for r in csv.DictReader(open(os.path.join(src, f"pmc_{c}_{tag}", "pmc_counter_collection.csv")))
-            if "flip_kernel" in r["Kernel_Name"]]
+            if "flip" in r["Kernel_Name"] and "kernel" in r["Kernel_Name"]]
+    kname = rows[0]["Kernel_Name"] if rows else None
     vals[c] = [float(r["Counter_Value"]) for r in rows]
 fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
 write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
 hbm = (2 * fetch + write) * 1024
-summary = {"round": tag, "kernel": "flip_kernel<8, 1, 2>", "chains": chains, "chain_steps": chain_steps,
+summary = {"round": tag, "kernel": kname, "chains": chains, "chain_steps": chain_steps,
            "FETCH_SIZE_KiB_per_launch": fetch, "WRITE_SIZE_KiB_per_launch": write,
            "launches": {k: len(v) for k, v in vals.items()},
            "hbm_bytes_per_launch": hbm,
