@@ -94,6 +94,51 @@ def from_networkx(g, pop_attr: str = "population", pos: Optional[Dict] = None) -
                      nx_graph=g, index=index)
 
 
+def from_json(src, pop_attr: str = "population", pos_attrs: Optional[Sequence[str]] = None) -> GraphSpec:
+    """A gerrychain / networkx JSON graph -> :class:`GraphSpec`.
+
+    ``src`` is a path, a file object or an already-parsed dict in networkx's
+    ``adjacency_data`` layout (what gerrychain ``Graph.to_json`` writes and ``Graph.from_json``
+    reads [gc-0.2]; ``networkx.readwrite.json_graph`` is imported by the reference at
+    ``grid_chain_sec11.py:12``) or its ``node_link_data`` layout.  List-valued node ids
+    (tuples after a JSON round trip) become tuples again.  Positions for the planar ring
+    builder come from ``pos_attrs`` (e.g. ``("C_X", "C_Y")``), else a ``pos`` attribute,
+    else 2-tuple node ids."""
+    import json
+    from networkx.readwrite import json_graph
+    if isinstance(src, dict):
+        data = src
+    elif hasattr(src, "read"):
+        data = json.load(src)
+    else:
+        with open(src) as f:
+            data = json.load(f)
+
+    def tup(x):
+        return tuple(tup(y) for y in x) if isinstance(x, list) else x
+
+    data = dict(data)
+    if "adjacency" in data:
+        data["nodes"] = [dict(nd, id=tup(nd["id"])) for nd in data["nodes"]]
+        data["adjacency"] = [[dict(e, id=tup(e["id"])) for e in row] for row in data["adjacency"]]
+        g = json_graph.adjacency_graph(data)
+    elif "links" in data or "edges" in data:
+        key = "links" if "links" in data else "edges"
+        data["nodes"] = [dict(nd, id=tup(nd["id"])) for nd in data["nodes"]]
+        data[key] = [dict(e, source=tup(e["source"]), target=tup(e["target"])) for e in data[key]]
+        g = json_graph.node_link_graph(data, edges=key) if key == "edges" else json_graph.node_link_graph(data)
+    else:
+        raise ValueError("from_json: neither an adjacency_data nor a node_link_data graph")
+    pos = None
+    if pos_attrs is not None:
+        pos = {nd: (float(g.nodes[nd][pos_attrs[0]]), float(g.nodes[nd][pos_attrs[1]])) for nd in g.nodes}
+    elif all("pos" in g.nodes[nd] for nd in g.nodes):
+        pos = {nd: tuple(float(x) for x in g.nodes[nd]["pos"]) for nd in g.nodes}
+    elif all(isinstance(nd, tuple) and len(nd) == 2 for nd in g.nodes):
+        pos = {nd: (float(nd[0]), float(nd[1])) for nd in g.nodes}
+    return from_networkx(g, pop_attr=pop_attr, pos=pos)
+
+
 # --------------------------------------------------------------------------------------
 # sec11 (grid_chain_sec11.py)
 # --------------------------------------------------------------------------------------

@@ -137,3 +137,25 @@ def test_ring_relation_is_symmetric(name):
     for v in range(spec.n):
         for x in R[v]:
             assert v in R[x], (v, x)
+
+
+def test_from_json_round_trips(tmp_path):
+    """gerrychain / networkx JSON ingestion gives the same CSR, populations
+    and positions as building from the networkx graph directly."""
+    import json
+    from networkx.readwrite import json_graph
+    from flipcomplexityempirical_amd import graphs as G
+    ref = G.sec11_graph()
+    g = G.sec11_nx()
+    for kind, data in (("adjacency", json_graph.adjacency_data(g)), ("node_link", json_graph.node_link_data(g))):
+        p = tmp_path / f"sec11_{kind}.json"
+        p.write_text(json.dumps(data))
+        spec = G.from_json(str(p))
+        assert spec.nodes == ref.nodes
+        assert np.array_equal(spec.row_ptr, ref.row_ptr) and np.array_equal(spec.col_idx, ref.col_idx)
+        assert np.array_equal(spec.pop, ref.pop) and np.array_equal(spec.pos, ref.pos)
+    # triangular lattice: positions from the 'pos' attribute
+    t = G.triangular_graph(6, 10)
+    data = json_graph.adjacency_data(t.nx_graph)
+    spec = G.from_json(data)
+    assert np.array_equal(spec.col_idx, t.col_idx) and np.allclose(spec.pos, t.pos)
