@@ -126,7 +126,7 @@ def from_json(src, pop_attr: str = "population", pos_attrs: Optional[Sequence[st
         key = "links" if "links" in data else "edges"
         data["nodes"] = [dict(nd, id=tup(nd["id"])) for nd in data["nodes"]]
         data[key] = [dict(e, source=tup(e["source"]), target=tup(e["target"])) for e in data[key]]
-        g = json_graph.node_link_graph(data, edges=key) if key == "edges" else json_graph.node_link_graph(data)
+        g = json_graph.node_link_graph(data, edges=key)
     else:
         raise ValueError("from_json: neither an adjacency_data nor a node_link_data graph")
     pos = None

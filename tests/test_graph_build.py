@@ -147,7 +147,7 @@ def test_from_json_round_trips(tmp_path):
     from flipcomplexityempirical_amd import graphs as G
     ref = G.sec11_graph()
     g = G.sec11_nx()
-    for kind, data in (("adjacency", json_graph.adjacency_data(g)), ("node_link", json_graph.node_link_data(g))):
+    for kind, data in (("adjacency", json_graph.adjacency_data(g)), ("node_link", json_graph.node_link_data(g, edges="links"))):
         p = tmp_path / f"sec11_{kind}.json"
         p.write_text(json.dumps(data))
         spec = G.from_json(str(p))
