@@ -23,6 +23,8 @@ FC_GRAPH_NO_EXACT = 0x1
 FC_PROPOSE_BI_SIGN, FC_PROPOSE_PAIR = 0, 1
 FC_DIAG_WAIT, FC_DIAG_HIST, FC_DIAG_EDGES, FC_DIAG_FLIPS, FC_DIAG_SERIES = 0x1, 0x2, 0x4, 0x8, 0x10
 FC_FLAG_FORCE_BFS = 0x1
+FC_ACCEPT_CUT, FC_ACCEPT_UNIFORM, FC_ACCEPT_ANNEAL = 0, 1, 2
+FC_CON_CONTIG, FC_CON_POP, FC_CON_BOUNDARY, FC_CON_FIXED, FC_CON_EMPTY = 0x1, 0x2, 0x4, 0x8, 0x100
 
 EXPORTED = [
     "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
@@ -47,7 +49,9 @@ class Params(ctypes.Structure):
                 ("flags", ctypes.c_uint32), ("device", ctypes.c_int32), ("trace_chains", ctypes.c_int32),
                 ("trace_cap", ctypes.c_int64), ("labels", _P(ctypes.c_int32)), ("log1mp", _P(ctypes.c_double)),
                 ("wmax", ctypes.c_int32), ("hit_lo", ctypes.c_int32), ("hit_hi", ctypes.c_int32),
-                ("event_cap", ctypes.c_int64)]
+                ("event_cap", ctypes.c_int64), ("accept", ctypes.c_int32), ("con_valid", ctypes.c_uint32),
+                ("con_accept", ctypes.c_uint32), ("beta", ctypes.c_double), ("frozen", _P(ctypes.c_int32)),
+                ("n_frozen", ctypes.c_int32)]
 
 
 class ChainStats(ctypes.Structure):

@@ -176,6 +176,85 @@ def always_accept(partition) -> bool:
     return True
 
 
+# ---- accept / constraint variants the reference builds but does not run ----
+
+
+def boundary_condition(partition) -> bool:
+    """``grid_chain_sec11.py:43-52``: some node of ``partition["boundary"]`` (the
+    ``boundary_node`` set, ``:228-234,292-297``) lies outside the district of the first."""
+    blist = partition["boundary"]
+    o_part = partition.assignment[blist[0]]
+    for x in blist:
+        if partition.assignment[x] != o_part:
+            return True
+    return False
+
+
+class FixedCutEdges:
+    """Constraint: the given edges stay cut.  ``fixed_endpoints`` (``:39-40``) is the
+    instance with the sec11 edges (19,0)-(20,0) and (19,39)-(20,39)."""
+
+    def __init__(self, pinned, name: str = "fixed_cut_edges"):
+        self.pinned = [tuple(e) for e in pinned]
+        self.__name__ = name
+
+    def __call__(self, partition) -> bool:
+        return all(partition.assignment[u] != partition.assignment[w] for u, w in self.pinned)
+
+
+fixed_endpoints = FixedCutEdges([((19, 0), (20, 0)), ((19, 39), (20, 39))], name="fixed_endpoints")
+
+
+class UniformAccept:
+    """``uniform_accept`` (``:159-165``): ``random() < 1`` iff ``popbound``,
+    ``single_flip_contiguous`` and ``boundary_condition`` hold, else ``< 0``.  The reference
+    reads its module-level ``popbound``; here it is the constructor argument, or the
+    Validator's population bound when the chain is compiled."""
+
+    __name__ = "uniform_accept"
+
+    def __init__(self, popbound=None):
+        self.popbound = popbound
+
+    def __call__(self, partition) -> bool:
+        if self.popbound is None:
+            raise ValueError("uniform_accept: no popbound given")
+        bound = 0
+        if self.popbound(partition) and single_flip_contiguous(partition) and boundary_condition(partition):
+            bound = 1
+        return random.random() < bound
+
+
+class AnnealingCutAcceptBackwards:
+    """``annealing_cut_accept_backwards`` (``:81-110``): ``random() < base ** (beta * (cut -
+    cut')) * |B'| / |B|`` (B = endpoints of the cut edges), 0 unless ``popbound`` and
+    ``single_flip_contiguous`` hold.  The reference fixes ``base = .1``, ``beta = 5``."""
+
+    __name__ = "annealing_cut_accept_backwards"
+
+    def __init__(self, popbound=None, base: float = .1, beta: float = 5):
+        self.popbound, self.base, self.beta = popbound, base, beta
+
+    def __call__(self, partition) -> bool:
+        if self.popbound is None:
+            raise ValueError("annealing_cut_accept_backwards: no popbound given")
+        b1 = {x[0] for x in partition["cut_edges"]} | {x[1] for x in partition["cut_edges"]}
+        b2 = {x[0] for x in partition.parent["cut_edges"]} | {x[1] for x in partition.parent["cut_edges"]}
+        bound = 1
+        if partition.parent is not None:
+            bound = (self.base ** (self.beta * (-len(partition["cut_edges"]) + len(partition.parent["cut_edges"])))) \
+                * (len(b1) / len(b2))
+            if not self.popbound(partition):
+                bound = 0
+            if not single_flip_contiguous(partition):
+                bound = 0
+        return random.random() < bound
+
+
+uniform_accept = UniformAccept()
+annealing_cut_accept_backwards = AnnealingCutAcceptBackwards()
+
+
 # ----------------------------------------------------------------------------------------
 # Partition
 # ----------------------------------------------------------------------------------------
@@ -246,6 +325,18 @@ class ChainSpec:
     pop_bounds_float: tuple
     contig_first: bool = True
     pop_key: str = "population"
+    accept: int = 0                 # FC_ACCEPT_*
+    con_valid: int = 0              # FC_CON_* of the Validator
+    con_accept: int = 0             # FC_CON_* of the accept callable
+    beta: float = 0.0
+    pinned: List[tuple] = field(default_factory=list)
+    frozen: List[int] = field(default_factory=list)
+    boundary_nodes: Optional[List[Hashable]] = None
+
+
+def _bounds_of(b) -> tuple:
+    lo_f, hi_f = b.bounds
+    return (lo_f, hi_f), (int(math.ceil(lo_f)), int(math.floor(hi_f)))
 
 
 def compile_chain(proposal, constraints, accept, initial_state: Partition) -> ChainSpec:
@@ -256,28 +347,56 @@ def compile_chain(proposal, constraints, accept, initial_state: Partition) -> Ch
     cons = constraints.constraints if isinstance(constraints, Validator) else (
         list(constraints) if isinstance(constraints, (list, tuple)) else [constraints])
     contig_idx, bounds, pop_key = None, None, "population"
+    con_valid, pinned = 0, []
     for i, c in enumerate(cons):
         nm = _name(c)
         if nm in ("single_flip_contiguous", "contiguous"):
             contig_idx = i
+            con_valid |= _lib.FC_CON_CONTIG
         elif isinstance(c, Bounds):
             if bounds is not None:
                 raise NotImplementedError("only one population Bounds constraint is supported")
             bounds = (i, c)
             pop_key = getattr(c, "pop_key", "population")
+            con_valid |= _lib.FC_CON_POP
+        elif nm == "boundary_condition":
+            con_valid |= _lib.FC_CON_BOUNDARY
+        elif isinstance(c, FixedCutEdges):
+            con_valid |= _lib.FC_CON_FIXED
+            pinned += c.pinned
         else:
             raise NotImplementedError(f"constraint {nm!r} is not implemented on the device")
-    if contig_idx is None:
-        raise NotImplementedError("the device chain always enforces single_flip_contiguous; include it")
     an = _name(accept)
+    acc_kind, con_accept, beta, acc_bounds = _lib.FC_ACCEPT_CUT, 0, 0.0, None
     if an == "cut_accept":
         if "base" not in initial_state.updaters:
             raise ValueError("cut_accept reads partition['base']: add the 'base' updater")
         base = float(initial_state["base"])
     elif an == "always_accept":
         base = 1.0
+    elif isinstance(accept, UniformAccept):
+        acc_kind, base = _lib.FC_ACCEPT_UNIFORM, 1.0
+        con_accept = _lib.FC_CON_CONTIG | _lib.FC_CON_POP | _lib.FC_CON_BOUNDARY
+        acc_bounds = accept.popbound
+    elif isinstance(accept, AnnealingCutAcceptBackwards):
+        acc_kind, base, beta = _lib.FC_ACCEPT_ANNEAL, float(accept.base), float(accept.beta)
+        con_accept = _lib.FC_CON_CONTIG | _lib.FC_CON_POP
+        acc_bounds = accept.popbound
     else:
-        raise NotImplementedError(f"accept {an!r}: the device implements cut_accept / always_accept")
+        raise NotImplementedError(f"accept {an!r}: the device implements cut_accept / always_accept / "
+                                  "uniform_accept / annealing_cut_accept_backwards")
+    if con_valid == 0:
+        con_valid = _lib.FC_CON_EMPTY  # Validator([]): nothing re-draws
+    if not ((con_valid | con_accept) & _lib.FC_CON_CONTIG):
+        raise NotImplementedError("the device chain keeps districts connected: single_flip_contiguous must be "
+                                  "in the Validator or the accept callable")
+    # one population bound on the device: the Validator's, the accept's, or both equal
+    if acc_bounds is None and (con_accept & _lib.FC_CON_POP):
+        if bounds is None:
+            raise NotImplementedError(f"{an}: give it a popbound (or a Bounds constraint in the Validator)")
+        acc_bounds = bounds[1]
+    if acc_bounds is not None and bounds is not None and tuple(acc_bounds.bounds) != tuple(bounds[1].bounds):
+        raise NotImplementedError("the Validator's and the accept callable's population bounds differ")
     g = initial_state.graph
     labels = sorted(set(initial_state.assignment.values()))
     if len(labels) != 2 or sorted(labels) != [-1, 1]:
@@ -288,14 +407,37 @@ def compile_chain(proposal, constraints, accept, initial_state: Partition) -> Ch
                          pos={n: (g.nodes[n]["pos"] if "pos" in g.nodes[n] else n) for n in g.nodes}
                          if all(isinstance(n, tuple) and len(n) == 2 for n in g.nodes) else None)
     init = spec.assignment_array(initial_state.assignment, labels)
-    if bounds is not None:
-        lo_f, hi_f = bounds[1].bounds
-        lo, hi = int(math.ceil(lo_f)), int(math.floor(hi_f))
-        contig_first = contig_idx < bounds[0]
+    pb = bounds[1] if bounds is not None else acc_bounds
+    if pb is not None:
+        (lo_f, hi_f), (lo, hi) = _bounds_of(pb)
+        contig_first = bounds is None or contig_idx is None or contig_idx < bounds[0]
     else:
         lo_f, hi_f, lo, hi, contig_first = -math.inf, math.inf, -(2 ** 31), 2 ** 31 - 1, True
+    frozen = sorted({spec.index[x] for e in pinned for x in e})
+    bnodes = None
+    if (con_valid | con_accept) & _lib.FC_CON_BOUNDARY:
+        if "boundary" not in initial_state.updaters:
+            raise ValueError("boundary_condition reads partition['boundary']: add the 'boundary' updater")
+        bnodes = list(initial_state["boundary"])
     return ChainSpec(spec=spec, labels=labels, init=init, base=base, pop_lo=lo, pop_hi=hi,
-                     pop_bounds_float=(lo_f, hi_f), contig_first=contig_first, pop_key=pop_key)
+                     pop_bounds_float=(lo_f, hi_f), contig_first=contig_first, pop_key=pop_key,
+                     accept=acc_kind, con_valid=con_valid, con_accept=con_accept, beta=beta, pinned=pinned,
+                     frozen=frozen, boundary_nodes=bnodes)
+
+
+def check_device_constraints(cs: ChainSpec, graph) -> None:
+    """Preconditions of the device forms of the variant constraints: ``boundary_condition``
+    is evaluated from the outer-face counts, so the boundary set must be the outer face;
+    ``fixed_endpoints`` freezes the pinned edges' endpoints, exact when the start plan cuts
+    every pinned edge (a k = 2 flip of an endpoint then always uncuts one)."""
+    if cs.boundary_nodes is not None:
+        _, meta = graph.rings()
+        outer = {cs.spec.nodes[i] for i in np.nonzero(meta & np.uint64(1 << 9))[0]}
+        if set(cs.boundary_nodes) != outer:
+            raise NotImplementedError("boundary_condition: the 'boundary' set must be the graph's outer face")
+    for u, w in cs.pinned:
+        if cs.init[cs.spec.index[u]] == cs.init[cs.spec.index[w]]:
+            raise NotImplementedError(f"fixed_endpoints: pinned edge {u}-{w} is not cut in the initial state")
 
 
 # ----------------------------------------------------------------------------------------
@@ -383,6 +525,10 @@ class MarkovChain:
         if failed:
             raise ValueError("The given initial_state is not valid according is_valid. "
                              "The failed constraints were: " + ",".join(failed))
+        if self.cspec.boundary_nodes is not None or self.cspec.pinned:
+            from .engine import FlipGraph
+            self._graph = FlipGraph(self.cspec.spec)
+            check_device_constraints(self.cspec, self._graph)
 
     def __len__(self):
         return self.total_steps
@@ -394,7 +540,9 @@ class MarkovChain:
         cfg = RunConfig(seed=self.seed, chain_id_offset=self.chain_id, pop_lo=self.cspec.pop_lo,
                         pop_hi=self.cspec.pop_hi, base=self.cspec.base, device=self.device, diag_mask=diag,
                         trace_chains=1 if trace else 0, trace_cap=64 * self.chunk + 4096 if trace else 0,
-                        labels=tuple(self.cspec.labels), event_cap=event_cap)
+                        labels=tuple(self.cspec.labels), event_cap=event_cap, accept=self.cspec.accept,
+                        con_valid=self.cspec.con_valid, con_accept=self.cspec.con_accept, beta=self.cspec.beta,
+                        frozen=tuple(self.cspec.frozen))
         return FlipRun(self._graph, self.cspec.init[None, :], cfg)
 
     # ---- per-step iteration (debugging path) -------------------------------------------

@@ -55,10 +55,12 @@ struct fc_run {
     int64_t *d_prof = nullptr;  // FC_PHASE_PROF builds
     int8_t *d_ser_a0 = nullptr;  // FC_DIAG_SERIES: assignment at the series window start
     char kname[96] = {0};        // last launched flip-kernel instance
+    bool variant = false;        // accept / constraint variants (FULL k = 2 instance)
 };
 
 namespace {
 
+constexpr int kWaveSlots = 64;
 thread_local std::string g_err;
 
 int fail(int code, const std::string &msg) {
@@ -215,6 +217,26 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: unsupported proposal");
     const fc::HostGraph &g = gr->h;
     const int32_t n = g.n, E = g.n_edges, R = g.ring_max, k = p->k;
+    // accept / constraint variants (uniform_accept, annealing_cut_accept_backwards,
+    // boundary_condition, fixed_endpoints: grid_chain_sec11.py:39-52,81-110,159-165)
+    const bool variant = p->accept != FC_ACCEPT_CUT || p->con_valid != 0 || p->con_accept != 0 || p->n_frozen > 0;
+    const uint32_t con_valid = p->con_valid ? p->con_valid : (FC_CON_CONTIG | FC_CON_POP);
+    const uint32_t con_all = FC_CON_CONTIG | FC_CON_POP | FC_CON_BOUNDARY | FC_CON_FIXED | FC_CON_EMPTY;
+    if (variant) {
+        if (k != 2) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: accept / constraint variants need k == 2");
+        if (p->accept < FC_ACCEPT_CUT || p->accept > FC_ACCEPT_ANNEAL)
+            return fail(FC_ERR_ARG, "fc_run_create: unknown accept kind");
+        if ((con_valid | p->con_accept) & ~con_all) return fail(FC_ERR_ARG, "fc_run_create: unknown constraint bits");
+        if (!((con_valid | p->con_accept) & FC_CON_CONTIG))
+            return fail(FC_ERR_UNSUPPORTED, "fc_run_create: single_flip_contiguous must be a Validator or accept "
+                                            "constraint (the device keeps districts connected)");
+        if (((con_valid | p->con_accept) & FC_CON_BOUNDARY) && g.n_gamma == 0)
+            return fail(FC_ERR_UNSUPPORTED, "fc_run_create: boundary_condition needs a planar graph with a simple "
+                                            "outer face (its nodes are the boundary set)");
+        if (p->n_frozen < 0 || (p->n_frozen > 0 && !p->frozen)) return fail(FC_ERR_ARG, "fc_run_create: frozen nodes");
+        for (int32_t i = 0; i < p->n_frozen; ++i)
+            if (p->frozen[i] < 0 || p->frozen[i] >= n) return fail(FC_ERR_ARG, "fc_run_create: frozen node out of range");
+    }
     if (p->pop_lo > INT32_MAX || p->pop_hi > INT32_MAX || p->pop_lo < INT32_MIN || p->pop_hi < INT32_MIN)
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: population bounds must fit int32");
     for (int64_t i = 0; i < (int64_t)n_chains * n; ++i)
@@ -235,6 +257,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         for (int32_t b = 0; b <= n; ++b) r->log1mp[b] = std::log(1.0 - (double)b / denom);
     }
     r->p.log1mp = nullptr;
+    r->p.frozen = nullptr;
+    r->p.con_valid = con_valid;
+    r->variant = variant;
     r->n_chains = n_chains;
     r->npad = (n + 15) & ~15;
     r->words = (n + 63) / 64;
@@ -275,10 +300,14 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
             pops[a[u]] += g.pop[u];
             if (g.meta[u] & fc::kMetaGamma) ng[a[u]] += 1;
         }
-        for (int d = 0; d < k; ++d)
-            if (pops[d] < p->pop_lo || pops[d] > p->pop_hi)
-                return fail(FC_ERR_INVALID_STATE, "chain " + std::to_string(c) +
-                                                      ": The given initial_state is not valid according is_valid (population).");
+        if (con_valid & FC_CON_POP)
+            for (int d = 0; d < k; ++d)
+                if (pops[d] < p->pop_lo || pops[d] > p->pop_hi)
+                    return fail(FC_ERR_INVALID_STATE, "chain " + std::to_string(c) +
+                                                          ": The given initial_state is not valid according is_valid (population).");
+        if ((con_valid & FC_CON_BOUNDARY) && (ng[0] == 0 || ng[1] == 0))
+            return fail(FC_ERR_INVALID_STATE, "chain " + std::to_string(c) +
+                                                  ": The given initial_state is not valid according is_valid (boundary_condition).");
         if (!district_contiguous(g, a, k, q, seen))
             return fail(FC_ERR_INVALID_STATE, "chain " + std::to_string(c) +
                                                   ": The given initial_state is not valid according is_valid (contiguity).");
@@ -325,6 +354,15 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
             for (int32_t u = 0; u < n; ++u) part_sum[(size_t)c * n + u] = r->labels[a[u]];  // :219
         const double base = bases ? bases[c] : p->base;
         for (int dd = -R; dd <= R; ++dd) {
+            if (p->accept == FC_ACCEPT_ANNEAL) {
+                // annealing_cut_accept_backwards, :99: base ** (beta * (-(cut' - cut))); the
+                // |B'| / |B| factor is applied on the device (the table holds the double)
+                const double bw = std::pow(base, p->beta * (double)(-dd));
+                uint64_t t;
+                std::memcpy(&t, &bw, 8);
+                thresh[(size_t)c * (2 * R + 1) + (dd + R)] = t;
+                continue;
+            }
             // cut_accept: random() < base ** (-(cut' - cut)), grid_chain_sec11.py:175,179
             const double bound = std::pow(base, (double)(-dd));
             uint64_t t;
@@ -341,10 +379,12 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     int rc;
     if (R == 8) {
         auto recs = pack_records<8>(g);
+        for (int32_t i = 0; i < p->n_frozen; ++i) recs[p->frozen[i]].meta |= fc::kMetaFrozen;
         if ((rc = dalloc((fc::NodeRec<8> **)&r->d_graph, recs.size()))) return rc;
         HIP_TRY(hipMemcpy(r->d_graph, recs.data(), recs.size() * sizeof(recs[0]), hipMemcpyHostToDevice));
     } else {
         auto recs = pack_records<16>(g);
+        for (int32_t i = 0; i < p->n_frozen; ++i) recs[p->frozen[i]].meta |= fc::kMetaFrozen;
         if ((rc = dalloc((fc::NodeRec<16> **)&r->d_graph, recs.size()))) return rc;
         HIP_TRY(hipMemcpy(r->d_graph, recs.data(), recs.size() * sizeof(recs[0]), hipMemcpyHostToDevice));
     }
@@ -474,6 +514,11 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     if (const char *e = std::getenv("FC_HIT_STOP")) k.hit_stop = std::atoi(e);
     k.par_min = 3;
     if (const char *e = std::getenv("FC_PAR_MIN")) k.par_min = std::atoi(e);
+    k.variant = r->variant ? 1 : 0;
+    k.accept = r->p.accept;
+    k.con_valid = r->p.con_valid;
+    k.con_accept = r->p.con_accept;
+    if (r->variant) k.par_min = kWaveSlots + 1;  // variants commit one event at a time
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : r->stream;
     k.prof = nullptr;
 #ifdef FC_PHASE_PROF

@@ -149,6 +149,7 @@ constexpr uint32_t LF_EXACT = 1u << 12;  // the run rule decides contiguity exac
 constexpr uint32_t LF_GAM = 1u << 13;    // outer-face node
 constexpr uint32_t LF_HAS = 1u << 14;    // the lane holds a slot
 constexpr uint32_t LF_WROTE = 1u << 15;  // the lane holds commit marks
+constexpr uint32_t LF_FRZ = 1u << 16;    // FC_CON_FIXED: the node may not flip
 
 }  // namespace dev
 }  // namespace fc

@@ -193,6 +193,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // would otherwise hold each as a 64-bit lane mask in SGPRs for the whole loop
         uint32_t st = (hit ? LF_HIT : 0u) | (acc ? LF_ACC : 0u) | (s_lin ? LF_SLIN : 0u) | (s_cyc ? LF_SCYC : 0u) |
                       (exact ? LF_EXACT : 0u) | (gam ? LF_GAM : 0u) | (has ? LF_HAS : 0u);
+        if (FULL && (rec.meta & kMetaFrozen)) st |= LF_FRZ;
         FC_STAMP(t_c);
         FC_PROF(2, t_c - t_b);
 
@@ -252,8 +253,45 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const bool ok = ((av ? ng0 : ng1) > 0) ? okT : okN;
             const int pa = av ? pops1 : pops0, pb = av ? pops0 : pops1;
             const bool popok = (pa - pv >= p.pop_lo) && (pb + pv <= p.pop_hi);
-            const bool valid = prop && known && ok && popok;
-            const uint64_t C0 = __ballot(valid && acc);
+            bool valid = prop && known && ok && popok;
+            bool acc_now = acc;
+            bool inv_contig = !ok;  // reason of an invalid proposal: contiguity, else "pop"
+            if constexpr (FULL) {
+                if (p.variant) {
+                    // Validator members re-draw, accept-callable constraints reject the step
+                    // (grid_chain_sec11.py:39-52,81-110,159-165); contiguity / populations as
+                    // above, boundary_condition from the outer-face counts, fixed_endpoints
+                    // from the frozen bit
+                    const int gm = gam ? 1 : 0;
+                    const bool b_ok = ((av ? ng1 : ng0) - gm > 0) && ((av ? ng0 : ng1) + gm > 0);
+                    const bool f_ok = !(st & LF_FRZ);
+                    auto pass = [&](uint32_t M) {
+                        return (!(M & FC_CON_CONTIG) || ok) && (!(M & FC_CON_POP) || popok) &&
+                               (!(M & FC_CON_BOUNDARY) || b_ok) && (!(M & FC_CON_FIXED) || f_ok);
+                    };
+                    valid = prop && known && pass(p.con_valid);
+                    inv_contig = (p.con_valid & FC_CON_CONTIG) && !ok;
+                    bool au = acc;
+                    if (p.accept == FC_ACCEPT_UNIFORM) {
+                        au = true;  // random() < 1
+                    } else if (p.accept == FC_ACCEPT_ANNEAL) {
+                        // bound = base ** (beta (cut - cut')) * (|B'| / |B|), :99; |B'| from the
+                        // foreign counts of v's neighbours (v stays a boundary node iff nA > 0)
+                        int dnb_l = nA == 0 ? -1 : 0;
+#pragma unroll
+                        for (int i = 0; i < RMAX; ++i) {
+                            const int oc = fcnt[cell[i]];
+                            const bool nb_i = (nbr >> i) & 1u;
+                            dnb_l += nb_i ? (int)(((inA >> i) & 1u) && oc == 0) - (int)(((tmask >> i) & 1u) && oc == 1) : 0;
+                        }
+                        const double bw = __longlong_as_double((long long)T[delta + RMAX]);
+                        const double bound = bw * ((double)(nb + dnb_l) / (double)nb);
+                        au = (double)mant53(w1, w2) * 0x1p-53 < bound;
+                    }
+                    acc_now = pass(p.con_accept) && au;
+                }
+            }
+            const uint64_t C0 = __ballot(valid && acc_now);
             if (__popcll(C0) >= p.par_min) {
                 FC_PROF(12, 1);
                 // ---- segment-parallel commit ---------------------------------------------
@@ -405,7 +443,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const int f = EV ? __builtin_ctzll(EV) : end;
             const uint64_t segv = VAL & bits_below(f);
             const int nvalid = __popcll(segv);
-            const uint32_t bits = valid ? ST_VS : (ok ? ST_IP : ST_IC);
+            const uint32_t bits = valid ? ST_VS : (inv_contig ? ST_IC : ST_IP);
             if (nvalid >= rem) {  // the launch's last step lies before f
                 const int e = kth_set_bit(segv, rem);
                 if (prop && lane <= e) st |= bits;
@@ -730,7 +768,7 @@ int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_
     const dim3 grid(blocks), block(kWave * wpb);
     // FULL: replay tapes, traces, event logs, histograms, per-node/per-edge tallies or a
     // hitting-time window; the lean instance keeps its registers for the hot loop.
-    const bool full = p.tape || p.trace || (p.diag & ~(uint32_t)FC_DIAG_WAIT) || p.hit_lo <= p.hit_hi;
+    const bool full = p.tape || p.trace || (p.diag & ~(uint32_t)FC_DIAG_WAIT) || p.hit_lo <= p.hit_hi || p.variant;
 #define FC_LAUNCH2(R, S, F)                                                                             \
     do {                                                                                                \
         if (lds > 65536)                                                                                \

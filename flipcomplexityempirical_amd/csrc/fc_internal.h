@@ -21,6 +21,7 @@ constexpr int kMaxKGeneral = 32;    // districts of the general (PAIR) kernel
 constexpr uint64_t kMetaLenMask = 0xffull;
 constexpr uint64_t kMetaExact = 1ull << 8;
 constexpr uint64_t kMetaGamma = 1ull << 9;
+constexpr uint64_t kMetaFrozen = 1ull << 10;  // FC_CON_FIXED: endpoint of a pinned cut edge (per run)
 constexpr int kMetaNbrShift = 16;
 constexpr int kMetaLinkShift = 32;
 
@@ -115,6 +116,10 @@ struct KParams {
     int32_t hit_stop;           // start another round only while fewer boundary hits than this
     int64_t *prof;              // [n_chains * kProfSlots] phase cycles (FC_PHASE_PROF builds only)
     int32_t par_min;            // k = 2: segment-parallel commit from this many acceptances on
+    int32_t variant;            // accept / constraint variants in use (FULL k = 2 instance)
+    int32_t accept;             // FC_ACCEPT_*
+    uint32_t con_valid;         // FC_CON_* of the Validator
+    uint32_t con_accept;        // FC_CON_* of the accept callable
 };
 
 // Diagnostic build (-DFC_PHASE_PROF): s_memtime cycles per kernel phase, per chain.

@@ -104,6 +104,12 @@ class RunConfig:
     hit_lo: int = 1          # hitting-time window on |cut| (hit_lo > hit_hi: off)
     hit_hi: int = 0
     event_cap: int = 0       # FC_DIAG_SERIES events kept per chain per window
+    # accept / constraint variants (k = 2; defaults: Validator([contiguous, popbound]) + cut_accept)
+    accept: int = _lib.FC_ACCEPT_CUT
+    con_valid: int = 0       # FC_CON_* of the Validator (0: CONTIG | POP)
+    con_accept: int = 0      # FC_CON_* tested by the accept callable
+    beta: float = 0.0        # FC_ACCEPT_ANNEAL exponent factor
+    frozen: Sequence[int] = ()  # FC_CON_FIXED: endpoints of the pinned edges
 
 
 class FlipRun:
@@ -136,7 +142,11 @@ class FlipRun:
                           flags=int(cfg.flags), device=int(cfg.device), trace_chains=int(cfg.trace_chains),
                           trace_cap=int(cfg.trace_cap), labels=_p(self._labels, ctypes.c_int32),
                           log1mp=_p(self._log1mp, ctypes.c_double), hit_lo=int(cfg.hit_lo),
-                          hit_hi=int(cfg.hit_hi), event_cap=int(cfg.event_cap))
+                          hit_hi=int(cfg.hit_hi), event_cap=int(cfg.event_cap), accept=int(cfg.accept),
+                          con_valid=int(cfg.con_valid), con_accept=int(cfg.con_accept), beta=float(cfg.beta))
+        self._frozen = np.ascontiguousarray(list(cfg.frozen), dtype=np.int32)
+        prm.frozen = _p(self._frozen, ctypes.c_int32)
+        prm.n_frozen = int(self._frozen.size)
         h = ctypes.c_void_p()
         check(L.fc_run_create(graph.handle, ctypes.byref(prm), self.n_chains, _p(self._init, ctypes.c_int8),
                               _p(self._bases, ctypes.c_double), ctypes.byref(h)), "fc_run_create")

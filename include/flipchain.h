@@ -54,6 +54,24 @@ extern "C" {
                                     series of :367-369 in run-length form; feeds
                                     fc_run_autocorr and the slope / angle series (:371-392)  */
 
+/* fc_params.accept: the accept callable (k = 2).  The variants are the reference's
+ * alternatives, built but unused by its sweeps.                           */
+#define FC_ACCEPT_CUT 0          /* cut_accept: random() < base ** (cut - cut'), :171-179     */
+#define FC_ACCEPT_UNIFORM 1      /* uniform_accept: 1 if its constraints hold, :159-165        */
+#define FC_ACCEPT_ANNEAL 2       /* annealing_cut_accept_backwards: random() <
+                                    base ** (beta (cut - cut')) * |B'| / |B|, :81-110          */
+
+/* Constraint sets (fc_params.con_valid / con_accept).  A constraint in con_valid is a
+ * Validator member: a proposal failing it is re-drawn (no step).  One in con_accept is
+ * tested inside the accept callable: failing it rejects the step (the state re-yields).  */
+#define FC_CON_CONTIG 0x1u       /* single_flip_contiguous                                  */
+#define FC_CON_POP 0x2u          /* within_percent_of_ideal_population (pop_lo / pop_hi)   */
+#define FC_CON_BOUNDARY 0x4u     /* boundary_condition, :43-52: both districts keep a node of
+                                    the outer face (the reference's boundary_node set)      */
+#define FC_CON_FIXED 0x8u        /* fixed_endpoints, :39-40: pinned edges stay cut; passed as
+                                    the pinned edges' endpoints (`frozen`), which may not flip */
+#define FC_CON_EMPTY 0x100u      /* con_valid: an empty Validator (0 selects CONTIG | POP)   */
+
 /* fc_params.flags */
 #define FC_FLAG_FORCE_BFS 0x1u   /* resolve every multi-run contiguity case by device BFS   */
 
@@ -90,6 +108,14 @@ typedef struct fc_params {
     int32_t hit_lo, hit_hi;    /* hitting time: first yield with hit_lo <= |cut| <= hit_hi
                                   (hit_lo > hit_hi: off)                                     */
     int64_t event_cap;         /* FC_DIAG_SERIES: events kept per chain per series window    */
+    /* accept / constraint variants (k = 2; all zero = Validator([single_flip_contiguous,
+       popbound]) + cut_accept, the reference's configuration)                               */
+    int32_t accept;            /* FC_ACCEPT_*                                                */
+    uint32_t con_valid;        /* FC_CON_* in the Validator (0 = CONTIG | POP)               */
+    uint32_t con_accept;       /* FC_CON_* tested by the accept callable                      */
+    double beta;               /* FC_ACCEPT_ANNEAL exponent factor (the reference: 5)       */
+    const int32_t *frozen;     /* FC_CON_FIXED: [n_frozen] endpoints of the pinned edges    */
+    int32_t n_frozen;
 } fc_params;
 
 /* Per-chain statistics.  "Yields" are the states a `for part in exp_chain` loop sees:

@@ -185,6 +185,46 @@ static void yield_state(ctx_t *c, fr_stats *st, fr_outputs *o, int64_t t) {
     }
 }
 
+/* boundary_condition (grid_chain_sec11.py:43-52) of the state with a[v] = T: some
+ * boundary node lies in another district than blist[0]. */
+static int boundary_ok_after(const ctx_t *c, int32_t v, int8_t T) {
+    const fr_params *p = c->p;
+    int32_t first = -1;
+    int8_t o_part = 0;
+    for (int32_t u = 0; u < p->n; ++u) {
+        if (!p->boundary[u]) continue;
+        const int8_t au = u == v ? T : c->a[u];
+        if (first < 0) { first = u; o_part = au; continue; }
+        if (au != o_part) return 1;
+    }
+    return 0;
+}
+
+/* fixed_endpoints (:39-40) of the state with a[v] = T: every pinned edge is cut. */
+static int fixed_ok_after(const ctx_t *c, int32_t v, int8_t T) {
+    const fr_params *p = c->p;
+    for (int32_t i = 0; i < p->n_pinned; ++i) {
+        const int32_t x = p->pinned[2 * i], y = p->pinned[2 * i + 1];
+        const int8_t ax = x == v ? T : c->a[x], ay = y == v ? T : c->a[y];
+        if (ax == ay) return 0;
+    }
+    return 1;
+}
+
+/* |b_nodes| of the state with a[v] = T, by flipping and restoring (the b_nodes of
+ * partition and partition.parent in annealing_cut_accept_backwards, :82-83). */
+static int32_t nb_after_flip(ctx_t *c, int32_t v, int8_t T) {
+    const fr_params *p = c->p;
+    int32_t before = in_boundary(c, v), after;
+    for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) before += in_boundary(c, p->col_idx[j]);
+    const int8_t A = c->a[v];
+    c->a[v] = T;
+    after = in_boundary(c, v);
+    for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) after += in_boundary(c, p->col_idx[j]);
+    c->a[v] = A;
+    return c->nb + after - before;
+}
+
 int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outputs *o) {
     if (!p || !init_assign || !st || p->n <= 0 || p->k < 2 || p->k > 64 || !p->row_ptr || !p->col_idx || !p->pop)
         return -2;
@@ -217,10 +257,16 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
         if (c.a[u] < 0 || c.a[u] >= p->k) { rc = -2; goto done; }
         c.pops[(int)c.a[u]] += p->pop[u];
     }
-    /* MarkovChain.__init__ validates the initial state [gc-0.2]. */
-    for (int32_t d = 0; d < p->k; ++d)
-        if (c.pops[d] < p->pop_lo || c.pops[d] > p->pop_hi) { rc = -1; goto done; }
+    /* MarkovChain.__init__ validates the initial state with the Validator [gc-0.2]; the
+     * districts must be connected in any case (the chain keeps them so). */
+    const uint32_t con_valid = p->con_valid ? p->con_valid : (FR_CON_CONTIG | FR_CON_POP);
+    if ((con_valid | p->con_accept) & FR_CON_BOUNDARY && !p->boundary) { rc = -2; goto done; }
+    if (con_valid & FR_CON_POP)
+        for (int32_t d = 0; d < p->k; ++d)
+            if (c.pops[d] < p->pop_lo || c.pops[d] > p->pop_hi) { rc = -1; goto done; }
     if (fr_districts_contiguous(n, p->row_ptr, p->col_idx, p->k, c.a) != 1) { rc = -1; goto done; }
+    if ((con_valid & FR_CON_BOUNDARY) && !boundary_ok_after(&c, 0, c.a[0])) { rc = -1; goto done; }
+    if ((con_valid & FR_CON_FIXED) && !fixed_ok_after(&c, 0, c.a[0])) { rc = -1; goto done; }
 
     for (int32_t e = 0; e < c.n_edges; ++e) c.cut += c.a[c.eu[e]] != c.a[c.ev[e]];
     for (int32_t u = 0; u < n; ++u) c.nb += in_boundary(&c, u);
@@ -288,14 +334,21 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
         }
         st->proposals += 1;
         int32_t flags = 0;
-        if (!flip_contiguous_ctx(&c, v)) {
-            st->inv_contig += 1; flags = 4;
-        } else {
-            for (int32_t dd = 0; dd < p->k; ++dd) {
-                int64_t pp = c.pops[dd] - (dd == A ? p->pop[v] : 0) + (dd == T ? p->pop[v] : 0);
-                if (pp < p->pop_lo || pp > p->pop_hi) { flags = 8; break; }
-            }
-            if (flags) st->inv_pop += 1;
+        /* constraint verdicts of the proposed state (Validator order: contiguity first) */
+        const int contig_ok = flip_contiguous_ctx(&c, v);
+        int pop_ok = 1;
+        for (int32_t dd = 0; dd < p->k; ++dd) {
+            int64_t pp = c.pops[dd] - (dd == A ? p->pop[v] : 0) + (dd == T ? p->pop[v] : 0);
+            if (pp < p->pop_lo || pp > p->pop_hi) { pop_ok = 0; break; }
+        }
+        const uint32_t all = (FR_CON_CONTIG | FR_CON_POP | FR_CON_BOUNDARY | FR_CON_FIXED) & (con_valid | p->con_accept);
+        const int bnd_ok = (all & FR_CON_BOUNDARY) ? boundary_ok_after(&c, v, T) : 1;
+        const int fix_ok = (all & FR_CON_FIXED) ? fixed_ok_after(&c, v, T) : 1;
+#define FR_PASS(M) ((!((M) & FR_CON_CONTIG) || contig_ok) && (!((M) & FR_CON_POP) || pop_ok) && \
+                    (!((M) & FR_CON_BOUNDARY) || bnd_ok) && (!((M) & FR_CON_FIXED) || fix_ok))
+        if (!FR_PASS(con_valid)) {
+            if ((con_valid & FR_CON_CONTIG) && !contig_ok) { st->inv_contig += 1; flags = 4; }
+            else { st->inv_pop += 1; flags = 8; }
         }
         if (flags) {
             if (o && o->trace && o->trace_len < o->trace_cap) {
@@ -312,7 +365,16 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
             same += aw == A; other += aw == T;
         }
         const int32_t delta = same - other;                    /* cut(S') - cut(S)        */
-        const double bound = pow(p->base, (double)(-delta));
+        double bound;
+        if (p->accept == FR_ACCEPT_UNIFORM) {          /* uniform_accept, :159-165 */
+            bound = FR_PASS(p->con_accept) ? 1.0 : 0.0;
+        } else if (p->accept == FR_ACCEPT_ANNEAL) {    /* annealing_cut_accept_backwards, :81-110 */
+            bound = pow(p->base, p->beta * (double)(-delta)) * ((double)nb_after_flip(&c, v, T) / (double)c.nb);
+            if (!FR_PASS(p->con_accept)) bound = 0.0;
+        } else {
+            bound = FR_PASS(p->con_accept) ? pow(p->base, (double)(-delta)) : 0.0;
+        }
+#undef FR_PASS
         const double U = u53(w[1], w[2]);
         const int acc = U < bound;
         if (acc) {

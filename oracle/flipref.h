@@ -80,7 +80,25 @@ typedef struct fr_params {
     const double *log1mp;      /* [n+1] log(1-|B|/(N^k-1)); NULL => waits are 0    */
     int32_t proposal;          /* FR_PROPOSE_BI_SIGN (k == 2) or FR_PROPOSE_PAIR   */
     int32_t wmax;              /* PAIR slot count (<= 0: min(max degree, k - 1))   */
+    /* accept / constraint variants (grid_chain_sec11.py:39-52,81-110,159-165); zero =
+     * Validator([single_flip_contiguous, popbound]) + cut_accept                           */
+    int32_t accept;            /* FR_ACCEPT_*                                      */
+    uint32_t con_valid;        /* FR_CON_* in the Validator (0: CONTIG | POP)      */
+    uint32_t con_accept;       /* FR_CON_* tested inside the accept callable       */
+    double beta;               /* annealing exponent factor                        */
+    const uint8_t *boundary;   /* [n] boundary_node flags (boundary_condition)     */
+    const int32_t *pinned;     /* [2 n_pinned] edges fixed_endpoints keeps cut     */
+    int32_t n_pinned;
 } fr_params;
+
+#define FR_ACCEPT_CUT 0        /* cut_accept                          :171-179 */
+#define FR_ACCEPT_UNIFORM 1    /* uniform_accept                      :159-165 */
+#define FR_ACCEPT_ANNEAL 2     /* annealing_cut_accept_backwards      :81-110  */
+#define FR_CON_CONTIG 1u       /* single_flip_contiguous                       */
+#define FR_CON_POP 2u          /* within_percent_of_ideal_population           */
+#define FR_CON_BOUNDARY 4u     /* boundary_condition                  :43-52   */
+#define FR_CON_FIXED 8u        /* fixed_endpoints                     :39-40   */
+#define FR_CON_EMPTY 0x100u    /* con_valid: an empty Validator                */
 
 #define FR_PROPOSE_BI_SIGN 0   /* slow_reversible_propose_bi, grid_chain_sec11.py:132-145 */
 #define FR_PROPOSE_PAIR 1      /* slow_reversible_propose,    grid_chain_sec11.py:117-130 */

@@ -109,7 +109,14 @@ class FrParams(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("chain_id", ctypes.c_uint32),
                 ("tape", _P(ctypes.c_uint32)), ("tape_draws", ctypes.c_int64),
                 ("n_steps", ctypes.c_int64), ("max_draws", ctypes.c_int64),
-                ("log1mp", _P(ctypes.c_double)), ("proposal", ctypes.c_int32), ("wmax", ctypes.c_int32)]
+                ("log1mp", _P(ctypes.c_double)), ("proposal", ctypes.c_int32), ("wmax", ctypes.c_int32),
+                ("accept", ctypes.c_int32), ("con_valid", ctypes.c_uint32), ("con_accept", ctypes.c_uint32),
+                ("beta", ctypes.c_double), ("boundary", _P(ctypes.c_uint8)), ("pinned", _P(ctypes.c_int32)),
+                ("n_pinned", ctypes.c_int32)]
+
+
+ACCEPT_CUT, ACCEPT_UNIFORM, ACCEPT_ANNEAL = 0, 1, 2
+CON_CONTIG, CON_POP, CON_BOUNDARY, CON_FIXED, CON_EMPTY = 1, 2, 4, 8, 0x100
 
 
 PROPOSE_BI_SIGN, PROPOSE_PAIR = 0, 1
@@ -174,7 +181,9 @@ class CRef:
             seed: int, chain_id: int, n_steps: int, k: int = 2, labels=(-1, 1),
             log1mp: Optional[np.ndarray] = None, tape: Optional[np.ndarray] = None,
             max_draws: int = 0, trace_cap: int = 0, want_hist: bool = False,
-            want_edges: bool = False, want_flips: bool = False, proposal: int = 0, wmax: int = 0) -> Dict:
+            want_edges: bool = False, want_flips: bool = False, proposal: int = 0, wmax: int = 0,
+            accept: int = 0, con_valid: int = 0, con_accept: int = 0, beta: float = 0.0,
+            boundary: Optional[np.ndarray] = None, pinned: Optional[np.ndarray] = None) -> Dict:
         n, E = spec.n, spec.n_edges
         row_ptr = np.ascontiguousarray(spec.row_ptr, dtype=np.int32)
         col_idx = np.ascontiguousarray(spec.col_idx, dtype=np.int32)
@@ -185,13 +194,17 @@ class CRef:
         init = np.ascontiguousarray(init_assign, dtype=np.int8)
         l1 = None if log1mp is None else np.ascontiguousarray(log1mp, dtype=np.float64)
         tp = None if tape is None else np.ascontiguousarray(tape, dtype=np.uint32)
+        bnd = None if boundary is None else np.ascontiguousarray(boundary, dtype=np.uint8)
+        pin = None if pinned is None else np.ascontiguousarray(pinned, dtype=np.int32).reshape(-1)
         p = FrParams(n=n, row_ptr=_ptr(row_ptr, ctypes.c_int32), col_idx=_ptr(col_idx, ctypes.c_int32),
                      pop=_ptr(pop, ctypes.c_int32), k=k, labels=_ptr(lab, ctypes.c_int32),
                      base=float(base), pop_lo=int(pop_lo), pop_hi=int(pop_hi), seed=int(seed),
                      chain_id=int(chain_id), tape=_ptr(tp, ctypes.c_uint32),
                      tape_draws=0 if tp is None else tp.shape[0] // 6,
                      n_steps=int(n_steps), max_draws=int(max_draws), log1mp=_ptr(l1, ctypes.c_double),
-                     proposal=int(proposal), wmax=int(wmax))
+                     proposal=int(proposal), wmax=int(wmax), accept=int(accept), con_valid=int(con_valid),
+                     con_accept=int(con_accept), beta=float(beta), boundary=_ptr(bnd, ctypes.c_uint8),
+                     pinned=_ptr(pin, ctypes.c_int32), n_pinned=0 if pin is None else pin.size // 2)
         trace = np.zeros(trace_cap, dtype=RECORD_DTYPE) if trace_cap else None
         final = np.zeros(n, dtype=np.int8)
         cut_hist = np.zeros(E + 1, dtype=np.int64) if want_hist else None

@@ -134,3 +134,30 @@ def test_bisection_plan_is_valid():
     assert pops.min() >= lo and pops.max() <= hi
     for d in range(18):
         assert nx.is_connected(spec.nx_graph.subgraph([n for n in spec.nodes if plan[n] == d]))
+
+
+def test_oracle_variants_respect_their_constraints(cref, sec11):
+    """The oracle's variant restatements keep what they promise: pinned edges stay cut,
+    both districts keep a boundary_node, and accept-side constraints reject (a rejected
+    step re-yields) instead of re-drawing."""
+    from flipcomplexityempirical_amd import graphs as G
+    from oracle import flipref as F
+    a0 = sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1])
+    _, (lo, hi) = G.population_bounds(sec11.n, 2, 0.1)
+    frame = np.asarray([1 if (0 in nd or 39 in nd) else 0 for nd in sec11.nodes], dtype=np.uint8)
+    pinned = np.asarray([(sec11.index[(19, 0)], sec11.index[(20, 0)]),
+                         (sec11.index[(19, 39)], sec11.index[(20, 39)])], dtype=np.int32)
+    r = cref.run(sec11, a0, base=1.0, pop_lo=lo, pop_hi=hi, seed=5, chain_id=0, n_steps=20000,
+                 accept=F.ACCEPT_CUT, con_valid=F.CON_CONTIG | F.CON_POP | F.CON_BOUNDARY | F.CON_FIXED,
+                 boundary=frame, pinned=pinned)
+    fin = r["final"]
+    assert all(fin[u] != fin[w] for u, w in pinned)
+    assert len(set(fin[frame == 1].tolist())) == 2
+    assert r["stats"]["accepted"] > 1000
+    # uniform_accept with an empty Validator: invalid proposals become rejected steps
+    r2 = cref.run(sec11, a0, base=1.0, pop_lo=lo, pop_hi=hi, seed=5, chain_id=0, n_steps=5000,
+                  accept=F.ACCEPT_UNIFORM, con_valid=F.CON_EMPTY, con_accept=F.CON_CONTIG | F.CON_POP | F.CON_BOUNDARY,
+                  boundary=frame)
+    s2 = r2["stats"]
+    assert s2["inv_contig"] == 0 and s2["inv_pop"] == 0 and s2["steps"] == s2["proposals"] == 5000
+    assert 0 < s2["accepted"] < 5000
