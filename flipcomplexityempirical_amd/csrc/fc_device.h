@@ -80,56 +80,135 @@ __device__ __forceinline__ bool one_run(uint32_t nbrA, uint32_t brk, uint32_t fu
     return cnt <= 1;
 }
 
-// Wave-cooperative BFS over the old district with v removed: are all old-district
-// neighbours of v (each lane < RMAX may hold one as its target) connected to `start`?
+// BFS scratch of one chain (LDS): 4-bit source labels of the visited nodes, the per-label
+// merge masks, and the frontier bitmaps.  Bitmaps are strided: node u is bit (u >> lsh) of
+// word (u & (W - 1)), W = 2^lsh words, so a spatially compact frontier (consecutive ids)
+// spreads over the lanes instead of queueing in one lane's word.
+struct BfsScratch {
+    uint32_t *lab;    // [(n + 7) / 8] nibbles: 0 unvisited, 1..15 source label
+    uint32_t *mm;     // [16] label i touched the labels in mm[i]
+    uint64_t *front;  // [W]
+    uint64_t *nxt;    // [W]
+    int lab_words;    // u32 words of lab
+    int lsh;          // log2 W
+};
+
+__device__ __forceinline__ uint32_t or_reduce(uint32_t x) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x |= (uint32_t)__shfl_xor((int)x, off);
+    return x;
+}
+
+// Multi-source wave BFS over the old district A with v removed (single_flip_contiguous
+// [gc-0.2], grid_chain_sec11.py:22,340): are all old-district neighbours of v connected?
+// Every neighbour (lane < RMAX holding it in my_target) starts its own labelled search;
+// searches that meet are merged (16-bit component masks, one per label, in lanes 0..15).
+// It answers yes once one component holds every label, and no once some component has
+// no frontier left -- it is then a whole connected piece of A - v without all of them,
+// which usually happens long before a single-source search would have exhausted A.
 template <int RMAX>
-__device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, uint64_t *vis, uint64_t *front,
-                         uint64_t *nxt, int words, int lane, int vf, int A, int my_target, int start,
-                         int64_t &levels) {
-    for (int i = lane; i < words; i += kWave) {
-        vis[i] = 0;
-        front[i] = 0;
-        nxt[i] = 0;
+__device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, const BfsScratch &S, int lane,
+                         int vf, int A, int my_target, int64_t &levels) {
+    const int W = 1 << S.lsh;
+    const uint32_t wm = (uint32_t)W - 1u;
+    for (int i = lane; i < S.lab_words; i += kWave) S.lab[i] = 0;
+    for (int i = lane; i < W; i += kWave) {
+        S.front[i] = 0;
+        S.nxt[i] = 0;
     }
+    if (lane < 16) S.mm[lane] = 0;
     wave_sync();
-    if (lane == 0) {
-        vis[vf >> 6] |= 1ull << (vf & 63);
-        vis[start >> 6] |= 1ull << (start & 63);
-        front[start >> 6] |= 1ull << (start & 63);
+    const bool src = my_target >= 0;
+    const uint64_t SM = __ballot(src);
+    const int ns = __popcll(SM);
+    if (ns <= 1) return true;
+    const uint32_t lab_me = src ? (uint32_t)(count_below(SM) + 1) : 0u;  // labels 1..ns
+    if (src) {
+        atomicOr(&S.lab[my_target >> 3], lab_me << ((my_target & 7) * 4));
+        atomicOr((unsigned long long *)&S.front[(uint32_t)my_target & wm], 1ull << (my_target >> S.lsh));
     }
+    const uint32_t all = ((1u << (ns + 1)) - 1u) & ~1u;  // labels 1..ns
+    uint32_t comp = lane < 16 ? (1u << lane) : 0u;      // component mask of label `lane`
     wave_sync();
     for (;;) {
         ++levels;
-        for (int i = lane; i < words; i += kWave) {
-            uint64_t bits = front[i];
+        uint32_t live = 0;  // labels that claimed a node at this level
+        bool merged = false;
+        for (int i = lane; i < W; i += kWave) {
+            uint64_t bits = S.front[i];
             while (bits) {
                 const int b = __builtin_ctzll(bits);
                 bits &= bits - 1;
-                const NodeRec<RMAX> r = G[i * 64 + b];
+                const int u = (b << S.lsh) | i;
+                const uint32_t la = (S.lab[u >> 3] >> ((u & 7) * 4)) & 15u;
+                const NodeRec<RMAX> r = G[u];
                 const uint32_t nbr = (uint32_t)(r.meta >> kMetaNbrShift) & 0xffffu;
 #pragma unroll
                 for (int j = 0; j < RMAX; ++j) {
                     if (!((nbr >> j) & 1u)) continue;
-                    const int e = ring_entry<RMAX>(r.ring, j);
-                    if (a[e] != A) continue;
-                    const uint64_t bit = 1ull << (e & 63);
-                    const uint64_t old = atomicOr((unsigned long long *)&vis[e >> 6], (unsigned long long)bit);
-                    if (!(old & bit)) atomicOr((unsigned long long *)&nxt[e >> 6], (unsigned long long)bit);
+                    const int w = ring_entry<RMAX>(r.ring, j);
+                    if (w == vf || a[w] != A) continue;
+                    uint32_t *wd = &S.lab[w >> 3];
+                    const int sh = (w & 7) * 4;
+                    uint32_t old = *wd;
+                    for (;;) {
+                        const uint32_t nib = (old >> sh) & 15u;
+                        if (nib) {
+                            if (nib != la) {
+                                atomicOr(&S.mm[la], 1u << nib);
+                                merged = true;
+                            }
+                            break;
+                        }
+                        const uint32_t prev = atomicCAS(wd, old, old | (la << sh));
+                        if (prev == old) {
+                            atomicOr((unsigned long long *)&S.nxt[(uint32_t)w & wm], 1ull << (w >> S.lsh));
+                            live |= 1u << la;
+                            break;
+                        }
+                        old = prev;
+                    }
                 }
             }
         }
         wave_sync();
-        const bool found = my_target < 0 || ((vis[my_target >> 6] >> (my_target & 63)) & 1ull);
-        if (__all(found)) return true;
+        if (__any(merged)) {
+            // comp(i) |= labels i touched, symmetric, then transitive closure (<= 4 rounds)
+            uint32_t adj = comp | (lane < 16 ? S.mm[lane] : 0u);
+            uint32_t sym = adj;
+#pragma unroll
+            for (int j = 1; j < 16; ++j) {
+                const uint32_t aj = (uint32_t)__shfl((int)adj, j);
+                if (lane < 16 && ((aj >> lane) & 1u)) sym |= 1u << j;
+            }
+            comp = lane < 16 ? sym : 0u;
+            for (int it = 0; it < 4; ++it) {
+                uint32_t nx = comp;
+#pragma unroll
+                for (int j = 1; j < 16; ++j) {
+                    const uint32_t cj = (uint32_t)__shfl((int)comp, j);
+                    if ((comp >> j) & 1u) nx |= cj;
+                }
+                const bool ch = nx != comp;
+                comp = nx;
+                if (!__any(ch)) break;
+            }
+            if (lane < 16) S.mm[lane] = 0;
+        }
+        if ((((uint32_t)__shfl((int)comp, 1)) & all) == all) return true;  // one component
+        live = or_reduce(live);
+        // a component without a live label is closed: a piece of A - v missing some label
+        const bool dead = lane >= 1 && lane <= ns && (comp & live) == 0u;
+        if (__any(dead)) return false;
         bool any = false;
-        for (int i = lane; i < words; i += kWave) {
-            const uint64_t x = nxt[i];
-            front[i] = x;
-            nxt[i] = 0;
+        for (int i = lane; i < W; i += kWave) {
+            const uint64_t x = S.nxt[i];
+            S.front[i] = x;
+            S.nxt[i] = 0;
             any |= x != 0;
         }
         wave_sync();
-        if (!__any(any)) return false;
+        if (!__any(any)) return false;  // unreachable: some label would be dead
     }
 }
 

@@ -49,10 +49,14 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     int8_t *a = (int8_t *)base;
     uint8_t *fcnt = base + npad;
     uint64_t *T = (uint64_t *)(base + 2 * npad);
-    uint64_t *vis = T + (2 * RMAX + 2);
-    uint64_t *front = vis + p.words;
-    uint64_t *nxt = front + p.words;
-    uint32_t *slot = (uint32_t *)(nxt + p.words);  // [5][64]: node, word1, word2, draw offset, word3
+    BfsScratch bs;                                  // BFS labels, merge masks, frontier bitmaps
+    bs.lab = (uint32_t *)(T + (2 * RMAX + 2));
+    bs.lab_words = p.lab_words;
+    bs.mm = bs.lab + p.lab_words;
+    bs.front = (uint64_t *)(bs.mm + 16);
+    bs.nxt = bs.front + p.words;
+    bs.lsh = p.bfs_lsh;
+    uint32_t *slot = (uint32_t *)(bs.nxt + p.words);  // [5][64]: node, word1, word2, draw offset, word3
     int32_t *popk = (int32_t *)(slot + 5 * 64);    // [32] district populations (KM = 0)
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
@@ -281,18 +285,16 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
         // contiguity undecided by the ring rule at slot f: wave BFS on the current state
         auto run_bfs = [&](int f) -> bool {
             const uint32_t pkf = rlu(pk, f), nbrAf = rlu(pk2, f) & rlu(pk2, f) >> 16;
-            int my_target = -1, start = -1;
+            int my_target = -1;
 #pragma unroll
             for (int k2 = 0; k2 < RMAX / 2; ++k2) {
                 const uint32_t wrd = rlu(rec.ring[k2], f);
                 if ((lane >> 1) == k2) my_target = (int)((wrd >> (16 * (lane & 1))) & 0xffffu);
-                if (start < 0 && ((nbrAf >> (2 * k2)) & 1u)) start = (int)(wrd & 0xffffu);
-                if (start < 0 && ((nbrAf >> (2 * k2 + 1)) & 1u)) start = (int)(wrd >> 16);
             }
             if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
             ++bfs_calls;
-            return wave_bfs<RMAX>(G, a, vis, front, nxt, p.words, lane, (int)(pkf & 0x7fffu),
-                                  (int)((pkf >> 15) & 63u), my_target, start, bfs_levels);
+            return wave_bfs<RMAX>(G, a, bs, lane, (int)(pkf & 0x7fffu), (int)((pkf >> 15) & 63u), my_target,
+                                  bfs_levels);
         };
         while (pos < end) {
             FC_PROF(6, 1);
