@@ -262,9 +262,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     r->variant = variant;
     r->n_chains = n_chains;
     r->npad = (n + 15) & ~15;
-    r->words = 1 << fc::bfs_lsh(n);
-    if (g.max_degree > 15)  // dev::wave_bfs labels each old neighbour with a 4-bit id
-        return fail(FC_ERR_UNSUPPORTED, "fc_run_create: node degree above 15");
+    r->words = (n + 63) / 64;
+    if (g.max_degree > 16)  // dev::wave_bfs labels each old neighbour with a 4-bit id
+        return fail(FC_ERR_UNSUPPORTED, "fc_run_create: node degree above 16");
     if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, BFS bitmaps, slots, commit marks (2 npad + 16)
         r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + fc::bfs_bytes(n) + 4 * 64 * 4 + 16;
     else         // fc_kernels.hip: a, fcnt, thresholds, BFS bitmaps, slots, district populations
@@ -478,7 +478,6 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.wthresh = (uint32_t)((1ull << 32) % (uint64_t)r->wmax);
     k.chain_lds_bytes = r->chain_lds_bytes;
     k.words = r->words;
-    k.bfs_lsh = fc::bfs_lsh(r->g.n);
     k.lab_words = fc::bfs_lab_words(r->g.n);
     k.lemire_thresh = (uint32_t)((1ull << 32) % (uint64_t)r->g.n);
     k.chain_id_offset = r->p.chain_id_offset;

@@ -80,17 +80,20 @@ __device__ __forceinline__ bool one_run(uint32_t nbrA, uint32_t brk, uint32_t fu
     return cnt <= 1;
 }
 
-// BFS scratch of one chain (LDS): 4-bit source labels of the visited nodes, the per-label
-// merge masks, and the frontier bitmaps.  Bitmaps are strided: node u is bit (u >> lsh) of
-// word (u & (W - 1)), W = 2^lsh words, so a spatially compact frontier (consecutive ids)
-// spreads over the lanes instead of queueing in one lane's word.
+// BFS scratch of one chain (LDS): 4-bit source labels of the visited nodes, per-label
+// merge and component masks, the visited / frontier bitmaps, and a compaction buffer that
+// deals each level's frontier out to the lanes in chunks of kBfsChunk nodes.
+constexpr int kBfsChunk = 256;
 struct BfsScratch {
-    uint32_t *lab;    // [(n + 7) / 8] nibbles: 0 unvisited, 1..15 source label
-    uint32_t *mm;     // [16] label i touched the labels in mm[i]
+    uint32_t *lab;    // [lab_words] nibbles: source label 0..15 of a visited node
+    uint32_t *mm;     // [16] labels that label i ran into this level
+    uint32_t *cm;     // [16] component mask of label i
+    uint16_t *list;   // [kBfsChunk] frontier chunk
+    uint64_t *vis;    // [W] visited
     uint64_t *front;  // [W]
     uint64_t *nxt;    // [W]
     int lab_words;    // u32 words of lab
-    int lsh;          // log2 W
+    int W;            // ceil(n / 64)
 };
 
 __device__ __forceinline__ uint32_t or_reduce(uint32_t x) {
@@ -102,82 +105,119 @@ __device__ __forceinline__ uint32_t or_reduce(uint32_t x) {
 // Multi-source wave BFS over the old district A with v removed (single_flip_contiguous
 // [gc-0.2], grid_chain_sec11.py:22,340): are all old-district neighbours of v connected?
 // Every neighbour (lane < RMAX holding it in my_target) starts its own labelled search;
-// searches that meet are merged (16-bit component masks, one per label, in lanes 0..15).
-// It answers yes once one component holds every label, and no once some component has
-// no frontier left -- it is then a whole connected piece of A - v without all of them,
-// which usually happens long before a single-source search would have exhausted A.
+// searches that meet are merged (16-bit component masks, one per label).  It answers yes
+// once one component holds every label, and no once some component has no frontier left
+// -- a whole connected piece of A - v without all of them -- which usually comes long
+// before a single-source search would have exhausted A.  Each level's frontier is
+// compacted (word popcounts + a wave prefix sum) and dealt out lane by lane.
 template <int RMAX>
-__device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, const BfsScratch &S, int lane,
-                         int vf, int A, int my_target, int64_t &levels) {
-    const int W = 1 << S.lsh;
-    const uint32_t wm = (uint32_t)W - 1u;
+__device__ __forceinline__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, const BfsScratch &S, int lane,
+                                         int vf, int A, int my_target, int64_t &levels) {
+    const int W = S.W;
     for (int i = lane; i < S.lab_words; i += kWave) S.lab[i] = 0;
     for (int i = lane; i < W; i += kWave) {
+        S.vis[i] = 0;
         S.front[i] = 0;
         S.nxt[i] = 0;
     }
-    if (lane < 16) S.mm[lane] = 0;
+    if (lane < 16) {
+        S.mm[lane] = 0;
+        S.cm[lane] = 1u << lane;
+    }
     wave_sync();
     const bool src = my_target >= 0;
     const uint64_t SM = __ballot(src);
-    const int ns = __popcll(SM);
+    const int ns = __popcll(SM);  // <= 16 (degree <= 16)
     if (ns <= 1) return true;
-    const uint32_t lab_me = src ? (uint32_t)(count_below(SM) + 1) : 0u;  // labels 1..ns
     if (src) {
+        const uint32_t lab_me = (uint32_t)count_below(SM);  // labels 0..ns-1
         atomicOr(&S.lab[my_target >> 3], lab_me << ((my_target & 7) * 4));
-        atomicOr((unsigned long long *)&S.front[(uint32_t)my_target & wm], 1ull << (my_target >> S.lsh));
+        atomicOr((unsigned long long *)&S.vis[my_target >> 6], 1ull << (my_target & 63));
+        atomicOr((unsigned long long *)&S.front[my_target >> 6], 1ull << (my_target & 63));
     }
-    const uint32_t all = ((1u << (ns + 1)) - 1u) & ~1u;  // labels 1..ns
-    uint32_t comp = lane < 16 ? (1u << lane) : 0u;      // component mask of label `lane`
+    if (lane == 0) atomicOr((unsigned long long *)&S.vis[vf >> 6], 1ull << (vf & 63));
+    const uint32_t all = (uint32_t)((1ull << ns) - 1ull);  // labels 0..ns-1
+    uint32_t comp = lane < 16 ? (1u << lane) : 0u;        // component mask of label `lane`
     wave_sync();
     for (;;) {
         ++levels;
         uint32_t live = 0;  // labels that claimed a node at this level
         bool merged = false;
-        for (int i = lane; i < W; i += kWave) {
-            uint64_t bits = S.front[i];
-            while (bits) {
-                const int b = __builtin_ctzll(bits);
-                bits &= bits - 1;
-                const int u = (b << S.lsh) | i;
+        // frontier size and each lane's first rank (lane owns words lane, lane + 64, ...)
+        int cnt = 0;
+        for (int i = lane; i < W; i += kWave) cnt += __popcll(S.front[i]);
+        const int incl = wave_scan_incl(cnt);
+        const int F = __builtin_amdgcn_readlane(incl, 63);
+#ifdef FC_PHASE_PROF
+        levels += F - 1;  // diagnostic build: count expanded nodes instead of levels
+#endif
+        for (int base = 0; base < F; base += kBfsChunk) {
+            int r = incl - cnt;
+            for (int i = lane; i < W && r < base + kBfsChunk; i += kWave) {
+                uint64_t bits = S.front[i];
+                const int pc = __popcll(bits);
+                if (r + pc <= base) {
+                    r += pc;
+                    continue;
+                }
+                while (bits) {
+                    const int b = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    if (r >= base && r < base + kBfsChunk) S.list[r - base] = (uint16_t)(i * 64 + b);
+                    ++r;
+                }
+            }
+            wave_sync();
+            const int m = min(kBfsChunk, F - base);
+            for (int q = lane; q < m; q += kWave) {
+                const int u = S.list[q];
                 const uint32_t la = (S.lab[u >> 3] >> ((u & 7) * 4)) & 15u;
-                const NodeRec<RMAX> r = G[u];
-                const uint32_t nbr = (uint32_t)(r.meta >> kMetaNbrShift) & 0xffffu;
+                const uint32_t cla = S.cm[la];
+                const NodeRec<RMAX> rr = G[u];
+                const uint32_t nbr = (uint32_t)(rr.meta >> kMetaNbrShift) & 0xffffu;
+                // three LDS round trips per node: claim every neighbour at once (vis bit:
+                // the first claimant wins), winners write their label, then losers read the
+                // labels they ran into (one wave: LDS in program order)
+                int wn[RMAX];
+                uint32_t cand = 0, won = 0;
 #pragma unroll
                 for (int j = 0; j < RMAX; ++j) {
-                    if (!((nbr >> j) & 1u)) continue;
-                    const int w = ring_entry<RMAX>(r.ring, j);
-                    if (w == vf || a[w] != A) continue;
-                    uint32_t *wd = &S.lab[w >> 3];
-                    const int sh = (w & 7) * 4;
-                    uint32_t old = *wd;
-                    for (;;) {
-                        const uint32_t nib = (old >> sh) & 15u;
-                        if (nib) {
-                            if (nib != la) {
-                                atomicOr(&S.mm[la], 1u << nib);
-                                merged = true;
-                            }
-                            break;
-                        }
-                        const uint32_t prev = atomicCAS(wd, old, old | (la << sh));
-                        if (prev == old) {
-                            atomicOr((unsigned long long *)&S.nxt[(uint32_t)w & wm], 1ull << (w >> S.lsh));
-                            live |= 1u << la;
-                            break;
-                        }
-                        old = prev;
+                    wn[j] = ring_entry<RMAX>(rr.ring, j);
+                    cand |= (uint32_t)(((nbr >> j) & 1u) && a[wn[j]] == A) << j;
+                }
+#pragma unroll
+                for (int j = 0; j < RMAX; ++j) {
+                    if (!((cand >> j) & 1u)) continue;
+                    const uint64_t bit = 1ull << (wn[j] & 63);
+                    const uint64_t old = atomicOr((unsigned long long *)&S.vis[wn[j] >> 6], bit);
+                    won |= (uint32_t)!(old & bit) << j;
+                }
+#pragma unroll
+                for (int j = 0; j < RMAX; ++j) {
+                    if (!((won >> j) & 1u)) continue;
+                    atomicOr(&S.lab[wn[j] >> 3], la << ((wn[j] & 7) * 4));
+                    atomicOr((unsigned long long *)&S.nxt[wn[j] >> 6], 1ull << (wn[j] & 63));
+                }
+                live |= won ? 1u << la : 0u;
+                compiler_fence();  // every winner's label store precedes the losers' reads
+#pragma unroll
+                for (int j = 0; j < RMAX; ++j) {
+                    if (!((cand & ~won) >> j & 1u) || wn[j] == vf) continue;
+                    const uint32_t nib = (S.lab[wn[j] >> 3] >> ((wn[j] & 7) * 4)) & 15u;
+                    if (!((cla >> nib) & 1u)) {  // another component
+                        atomicOr(&S.mm[la], 1u << nib);
+                        merged = true;
                     }
                 }
             }
+            wave_sync();
         }
-        wave_sync();
         if (__any(merged)) {
             // comp(i) |= labels i touched, symmetric, then transitive closure (<= 4 rounds)
-            uint32_t adj = comp | (lane < 16 ? S.mm[lane] : 0u);
+            const uint32_t adj = comp | (lane < 16 ? S.mm[lane] : 0u);
             uint32_t sym = adj;
 #pragma unroll
-            for (int j = 1; j < 16; ++j) {
+            for (int j = 0; j < 16; ++j) {
                 const uint32_t aj = (uint32_t)__shfl((int)adj, j);
                 if (lane < 16 && ((aj >> lane) & 1u)) sym |= 1u << j;
             }
@@ -185,7 +225,7 @@ __device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, c
             for (int it = 0; it < 4; ++it) {
                 uint32_t nx = comp;
 #pragma unroll
-                for (int j = 1; j < 16; ++j) {
+                for (int j = 0; j < 16; ++j) {
                     const uint32_t cj = (uint32_t)__shfl((int)comp, j);
                     if ((comp >> j) & 1u) nx |= cj;
                 }
@@ -193,13 +233,66 @@ __device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, c
                 comp = nx;
                 if (!__any(ch)) break;
             }
-            if (lane < 16) S.mm[lane] = 0;
+            if (lane < 16) {
+                S.mm[lane] = 0;
+                S.cm[lane] = comp;
+            }
         }
-        if ((((uint32_t)__shfl((int)comp, 1)) & all) == all) return true;  // one component
+        if ((((uint32_t)__shfl((int)comp, 0)) & all) == all) return true;  // one component
         live = or_reduce(live);
         // a component without a live label is closed: a piece of A - v missing some label
-        const bool dead = lane >= 1 && lane <= ns && (comp & live) == 0u;
+        const bool dead = lane < ns && (comp & live) == 0u;
         if (__any(dead)) return false;
+        for (int i = lane; i < W; i += kWave) {
+            S.front[i] = S.nxt[i];
+            S.nxt[i] = 0;
+        }
+        wave_sync();
+    }
+}
+
+// Register-light single-source form for the k = 2 kernel, where the planar rule decides
+// every node of the reference's lattices and the search is the rare fallback: are all
+// old-district neighbours (lanes < RMAX hold them in my_target) reached from `start`?
+template <int RMAX>
+__device__ bool wave_bfs_single(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, const BfsScratch &S,
+                                int lane, int vf, int A, int my_target, int start, int64_t &levels) {
+    const int W = S.W;
+    for (int i = lane; i < W; i += kWave) {
+        S.vis[i] = 0;
+        S.front[i] = 0;
+        S.nxt[i] = 0;
+    }
+    wave_sync();
+    if (lane == 0) {
+        S.vis[vf >> 6] |= 1ull << (vf & 63);
+        S.vis[start >> 6] |= 1ull << (start & 63);
+        S.front[start >> 6] |= 1ull << (start & 63);
+    }
+    wave_sync();
+    for (;;) {
+        ++levels;
+        for (int i = lane; i < W; i += kWave) {
+            uint64_t bits = S.front[i];
+            while (bits) {
+                const int b = __builtin_ctzll(bits);
+                bits &= bits - 1;
+                const NodeRec<RMAX> r = G[i * 64 + b];
+                const uint32_t nbr = (uint32_t)(r.meta >> kMetaNbrShift) & 0xffffu;
+#pragma unroll
+                for (int j = 0; j < RMAX; ++j) {
+                    if (!((nbr >> j) & 1u)) continue;
+                    const int e = ring_entry<RMAX>(r.ring, j);
+                    if (a[e] != A) continue;
+                    const uint64_t bit = 1ull << (e & 63);
+                    const uint64_t old = atomicOr((unsigned long long *)&S.vis[e >> 6], (unsigned long long)bit);
+                    if (!(old & bit)) atomicOr((unsigned long long *)&S.nxt[e >> 6], (unsigned long long)bit);
+                }
+            }
+        }
+        wave_sync();
+        const bool found = my_target < 0 || ((S.vis[my_target >> 6] >> (my_target & 63)) & 1ull);
+        if (__all(found)) return true;
         bool any = false;
         for (int i = lane; i < W; i += kWave) {
             const uint64_t x = S.nxt[i];
@@ -208,7 +301,7 @@ __device__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, c
             any |= x != 0;
         }
         wave_sync();
-        if (!__any(any)) return false;  // unreachable: some label would be dead
+        if (!__any(any)) return false;
     }
 }
 

@@ -47,13 +47,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     int8_t *a = (int8_t *)base;                    // [npad] district of each node
     uint8_t *fcnt = base + npad;                   // [npad] foreign neighbours of each node
     uint64_t *T = (uint64_t *)(base + 2 * npad);   // [2 RMAX + 2] acceptance thresholds by delta-cut
-    BfsScratch bs;                                  // BFS labels, merge masks, frontier bitmaps
+    BfsScratch bs;                                  // BFS labels, masks, chunk, bitmaps
     bs.lab = (uint32_t *)(T + (2 * RMAX + 2));
     bs.lab_words = p.lab_words;
     bs.mm = bs.lab + p.lab_words;
-    bs.front = (uint64_t *)(bs.mm + 16);
+    bs.cm = bs.mm + 16;
+    bs.list = (uint16_t *)(bs.cm + 16);
+    bs.vis = (uint64_t *)(bs.list + kBfsChunk);
+    bs.front = bs.vis + p.words;
     bs.nxt = bs.front + p.words;
-    bs.lsh = p.bfs_lsh;
+    bs.W = p.words;
     uint32_t *slot = (uint32_t *)(bs.nxt + p.words);  // [4][64]: node, word1, word2, draw offset
     uint8_t *smark = (uint8_t *)(slot + 4 * 64);   // [npad] lowest slot of a segment flip at the node
     uint8_t *nmark = smark + npad;                 // [npad] ... having the node as a neighbour
@@ -216,15 +219,17 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // contiguity undecided by the ring rule at lane f: wave BFS on the current state
         auto run_bfs = [&](int f) -> bool {
             const uint32_t nbrAf = rlu(nbrA, f);
-            int my_target = -1;
+            int my_target = -1, start = -1;
 #pragma unroll
             for (int k2 = 0; k2 < RMAX / 2; ++k2) {
                 const uint32_t wrd = rlu(rec.ring[k2], f);
                 if ((lane >> 1) == k2) my_target = (int)((wrd >> (16 * (lane & 1))) & 0xffffu);
+                if (start < 0 && ((nbrAf >> (2 * k2)) & 1u)) start = (int)(wrd & 0xffffu);
+                if (start < 0 && ((nbrAf >> (2 * k2 + 1)) & 1u)) start = (int)(wrd >> 16);
             }
             if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
             ++bfs_calls;
-            return wave_bfs<RMAX>(G, a, bs, lane, rl32(v, f), rl32(av, f), my_target, bfs_levels);
+            return wave_bfs_single<RMAX>(G, a, bs, lane, rl32(v, f), rl32(av, f), my_target, start, bfs_levels);
         };
 
         while (pos < end) {

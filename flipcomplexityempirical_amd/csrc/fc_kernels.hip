@@ -49,13 +49,16 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     int8_t *a = (int8_t *)base;
     uint8_t *fcnt = base + npad;
     uint64_t *T = (uint64_t *)(base + 2 * npad);
-    BfsScratch bs;                                  // BFS labels, merge masks, frontier bitmaps
+    BfsScratch bs;                                  // BFS labels, masks, chunk, bitmaps
     bs.lab = (uint32_t *)(T + (2 * RMAX + 2));
     bs.lab_words = p.lab_words;
     bs.mm = bs.lab + p.lab_words;
-    bs.front = (uint64_t *)(bs.mm + 16);
+    bs.cm = bs.mm + 16;
+    bs.list = (uint16_t *)(bs.cm + 16);
+    bs.vis = (uint64_t *)(bs.list + kBfsChunk);
+    bs.front = bs.vis + p.words;
     bs.nxt = bs.front + p.words;
-    bs.lsh = p.bfs_lsh;
+    bs.W = p.words;
     uint32_t *slot = (uint32_t *)(bs.nxt + p.words);  // [5][64]: node, word1, word2, draw offset, word3
     int32_t *popk = (int32_t *)(slot + 5 * 64);    // [32] district populations (KM = 0)
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
@@ -293,8 +296,13 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
             }
             if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
             ++bfs_calls;
-            return wave_bfs<RMAX>(G, a, bs, lane, (int)(pkf & 0x7fffu), (int)((pkf >> 15) & 63u), my_target,
-                                  bfs_levels);
+            FC_STAMP(t_b0);
+            const bool res = wave_bfs<RMAX>(G, a, bs, lane, (int)(pkf & 0x7fffu), (int)((pkf >> 15) & 63u), my_target,
+                                            bfs_levels);
+            FC_STAMP(t_b1);
+            FC_PROF(13, t_b1 - t_b0);
+            FC_PROF(14, 1);
+            return res;
         };
         while (pos < end) {
             FC_PROF(6, 1);
