@@ -20,7 +20,7 @@ FC_ERR_UNSUPPORTED = -4
 FC_ERR_NOMEM = -5
 
 FC_GRAPH_NO_EXACT = 0x1
-FC_PROPOSE_BI_SIGN, FC_PROPOSE_PAIR = 0, 1
+FC_PROPOSE_BI_SIGN, FC_PROPOSE_PAIR, FC_PROPOSE_RECOM = 0, 1, 2
 FC_DIAG_WAIT, FC_DIAG_HIST, FC_DIAG_EDGES, FC_DIAG_FLIPS, FC_DIAG_SERIES = 0x1, 0x2, 0x4, 0x8, 0x10
 FC_FLAG_FORCE_BFS = 0x1
 FC_ACCEPT_CUT, FC_ACCEPT_UNIFORM, FC_ACCEPT_ANNEAL = 0, 1, 2
@@ -29,7 +29,8 @@ FC_CON_CONTIG, FC_CON_POP, FC_CON_BOUNDARY, FC_CON_FIXED, FC_CON_EMPTY = 0x1, 0x
 EXPORTED = [
     "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
     "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
-    "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_trace_reset", "fc_run_read_hist",
+    "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_read_recom_trace",
+    "fc_run_trace_reset", "fc_run_read_hist",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
     "fc_run_frame_series", "fc_run_kernel_name", "fc_run_n_chains", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
@@ -51,7 +52,9 @@ class Params(ctypes.Structure):
                 ("wmax", ctypes.c_int32), ("hit_lo", ctypes.c_int32), ("hit_hi", ctypes.c_int32),
                 ("event_cap", ctypes.c_int64), ("accept", ctypes.c_int32), ("con_valid", ctypes.c_uint32),
                 ("con_accept", ctypes.c_uint32), ("beta", ctypes.c_double), ("frozen", _P(ctypes.c_int32)),
-                ("n_frozen", ctypes.c_int32)]
+                ("n_frozen", ctypes.c_int32), ("recom_pop_target", ctypes.c_double),
+                ("recom_epsilon", ctypes.c_double), ("recom_node_repeats", ctypes.c_int32),
+                ("recom_max_attempts", ctypes.c_int32)]
 
 
 class ChainStats(ctypes.Structure):
@@ -73,6 +76,12 @@ class Event(ctypes.Structure):
 class Record(ctypes.Structure):
     _fields_ = [("draw", ctypes.c_int64), ("v", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("cut", ctypes.c_int32), ("nb", ctypes.c_int32), ("wait", ctypes.c_int64)]
+
+
+class RecomRecord(ctypes.Structure):
+    _fields_ = [("draw", ctypes.c_int64), ("edge", ctypes.c_int32), ("root", ctypes.c_int32),
+                ("child", ctypes.c_int32), ("attempts", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("cut", ctypes.c_int32)]
 
 
 class FlipChainError(RuntimeError):
@@ -117,6 +126,7 @@ def load(build_if_missing: bool = True):
     L.fc_run_read_state.argtypes = [vp, _P(ctypes.c_int8)]
     L.fc_run_read_pops.argtypes = [vp, _P(i64)]
     L.fc_run_read_trace.argtypes = [vp, i32, _P(Record), i64, _P(i64)]
+    L.fc_run_read_recom_trace.argtypes = [vp, i32, _P(RecomRecord), i64, _P(i64)]
     L.fc_run_trace_reset.argtypes = [vp]
     L.fc_run_read_hist.argtypes = [vp, _P(i64), _P(i64)]
     L.fc_run_read_edges.argtypes = [vp, _P(i64)]

@@ -53,6 +53,8 @@ struct fc_run {
     uint32_t *d_tape = nullptr;
     int64_t tape_draws = 0;
     int64_t *d_prof = nullptr;  // FC_PHASE_PROF builds
+    int32_t *d_eu = nullptr, *d_ev = nullptr;  // recom: canonical edge list
+    uint64_t *d_recom_thresh = nullptr;        // recom: [2E+1] acceptance thresholds
     int8_t *d_ser_a0 = nullptr;  // FC_DIAG_SERIES: assignment at the series window start
     char kname[96] = {0};        // last launched flip-kernel instance
     bool variant = false;        // accept / constraint variants (FULL k = 2 instance)
@@ -87,7 +89,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc, r->d_edge_since,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events, r->d_prof, r->d_ser_a0};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events, r->d_prof, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -213,8 +215,20 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: k must be in [2, 32]");
     if (p->proposal == FC_PROPOSE_BI_SIGN && p->k != 2)
         return fail(FC_ERR_ARG, "fc_run_create: slow_reversible_propose_bi flips between two districts (k == 2)");
-    if (p->proposal != FC_PROPOSE_BI_SIGN && p->proposal != FC_PROPOSE_PAIR)
+    if (p->proposal != FC_PROPOSE_BI_SIGN && p->proposal != FC_PROPOSE_PAIR && p->proposal != FC_PROPOSE_RECOM)
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: unsupported proposal");
+    const bool recom = p->proposal == FC_PROPOSE_RECOM;
+    if (recom) {
+        if (p->accept != FC_ACCEPT_CUT || p->con_valid != 0 || p->con_accept != 0 || p->n_frozen > 0)
+            return fail(FC_ERR_UNSUPPORTED, "fc_run_create: recom runs with the population Validator and cut_accept");
+        if (!(p->recom_epsilon >= 0.0) || !(p->recom_pop_target > 0.0))
+            return fail(FC_ERR_ARG, "fc_run_create: recom needs pop_target > 0 and epsilon >= 0");
+        if (gr->h.n > 8000)
+            return fail(FC_ERR_UNSUPPORTED, "fc_run_create: recom keeps a chain's spanning tree in LDS (n <= 8000)");
+        if (bases)
+            for (int32_t c = 1; c < n_chains; ++c)
+                if (bases[c] != bases[0]) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: recom takes one base");
+    }
     const fc::HostGraph &g = gr->h;
     const int32_t n = g.n, E = g.n_edges, R = g.ring_max, k = p->k;
     // accept / constraint variants (uniform_accept, annealing_cut_accept_backwards,
@@ -265,7 +279,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     r->words = (n + 63) / 64;
     if (g.max_degree > 16)  // dev::wave_bfs labels each old neighbour with a 4-bit id
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: node degree above 16");
-    if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, BFS bitmaps, slots, commit marks (2 npad + 16)
+    if (recom)   // fc_recom.hip: best / spop, tree slots, component / levels, order, parent, a
+        r->chain_lds_bytes = fc::recom_lds_bytes(n);
+    else if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, BFS bitmaps, slots, commit marks (2 npad + 16)
         r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + fc::bfs_bytes(n) + 4 * 64 * 4 + 16;
     else         // fc_kernels.hip: a, fcnt, thresholds, BFS bitmaps, slots, district populations
         r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + fc::bfs_bytes(n) + 5 * 64 * 4 + fc::kMaxKGeneral * 4;
@@ -435,6 +451,23 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     } else {
         r->p.diag_mask &= ~FC_DIAG_SERIES;
     }
+    if (recom) {
+        if ((rc = dalloc(&r->d_eu, (size_t)std::max(E, 1)))) return rc;
+        if ((rc = dalloc(&r->d_ev, (size_t)std::max(E, 1)))) return rc;
+        if (E) {
+            HIP_TRY(hipMemcpy(r->d_eu, g.eu.data(), (size_t)E * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(r->d_ev, g.ev.data(), (size_t)E * 4, hipMemcpyHostToDevice));
+        }
+        // cut_accept: random() < base ** (cut - cut'), cut - cut' in [-E, E]
+        const double rb = bases ? bases[0] : p->base;
+        std::vector<uint64_t> th(2 * (size_t)E + 1);
+        for (int32_t dd = -E; dd <= E; ++dd) {
+            const double bound = std::pow(rb, (double)dd);
+            th[dd + E] = !(bound < 1.0) ? (1ull << 53) : !(bound > 0.0) ? 0 : (uint64_t)std::ceil(bound * 9007199254740992.0);
+        }
+        if ((rc = dalloc(&r->d_recom_thresh, th.size()))) return rc;
+        HIP_TRY(hipMemcpy(r->d_recom_thresh, th.data(), th.size() * 8, hipMemcpyHostToDevice));
+    }
     if (p->trace_chains > 0 && p->trace_cap > 0) {
         const int32_t tc = std::min(p->trace_chains, n_chains);
         r->p.trace_chains = tc;
@@ -539,6 +572,42 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     }
     auto &evp = r->launch_events[r->n_launch_events];
     HIP_TRY(hipEventRecord(evp.first, s));
+    if (r->p.proposal == FC_PROPOSE_RECOM) {
+        fc::RecomParams q{};
+        q.graph = r->d_graph;
+        q.ring_eid = r->d_ring_eid;
+        q.eu = r->d_eu;
+        q.ev = r->d_ev;
+        q.n = r->g.n;
+        q.n_edges = r->g.n_edges;
+        q.n_chains = r->n_chains;
+        q.chain_lds_bytes = r->chain_lds_bytes;
+        q.chain_id_offset = r->p.chain_id_offset;
+        q.seed_lo = (uint32_t)r->p.seed;
+        q.seed_hi = (uint32_t)(r->p.seed >> 32);
+        q.pop_lo = (int32_t)r->p.pop_lo;
+        q.pop_hi = (int32_t)r->p.pop_hi;
+        q.pop_target = r->p.recom_pop_target;
+        q.epsilon = r->p.recom_epsilon;
+        q.node_repeats = r->p.recom_node_repeats > 0 ? r->p.recom_node_repeats : 1;
+        q.max_attempts = r->p.recom_max_attempts > 0 ? r->p.recom_max_attempts : 10000;
+        q.n_steps = n_steps;
+        q.max_draws = max_draws > 0 ? max_draws : 1024 * std::max<int64_t>(n_steps, 1);
+        q.assign = r->d_assign;
+        q.sc = r->d_sc;
+        q.accept_thresh = r->d_recom_thresh;
+        q.trace = (fc_recom_record *)r->d_trace;
+        q.trace_chains = r->p.trace_chains;
+        q.trace_cap = r->p.trace_cap;
+        const int e = fc::launch_recom(q, r->g.ring_max, s, r->kname, sizeof r->kname);
+        if (e != 0) return fail(FC_ERR_HIP, std::string("recom kernel launch: ") + hipGetErrorString((hipError_t)e));
+        HIP_TRY(hipEventRecord(evp.second, s));
+        r->ev0 = evp.first;
+        r->ev1 = evp.second;
+        ++r->n_launch_events;
+        r->timed = true;
+        return FC_OK;
+    }
     // the kernel keeps per-launch step and per-lane counters in 32 bits: launch in chunks
     constexpr int64_t kChunk = int64_t(1) << 24;
     for (int64_t done = 0; done < n_steps; done += kChunk) {
@@ -671,6 +740,21 @@ int fc_run_read_trace(fc_run *r, int32_t chain, fc_record *out, int64_t cap, int
     const int64_t n = std::min<int64_t>({s.trace_len, r->p.trace_cap, cap});
     HIP_TRY(hipMemcpy(out, r->d_trace + (size_t)chain * r->p.trace_cap, (size_t)n * sizeof(fc_record),
                       hipMemcpyDeviceToHost));
+    *len = s.trace_len;
+    return FC_OK;
+}
+
+int fc_run_read_recom_trace(fc_run *r, int32_t chain, fc_recom_record *out, int64_t cap, int64_t *len) {
+    if (!r || !out || !len) return fail(FC_ERR_ARG, "fc_run_read_recom_trace: null argument");
+    if (r->p.proposal != FC_PROPOSE_RECOM) return fail(FC_ERR_ARG, "fc_run_read_recom_trace: not a recom run");
+    if (chain < 0 || chain >= r->p.trace_chains) return fail(FC_ERR_ARG, "fc_run_read_recom_trace: chain is not traced");
+    if (int rc = fc_run_sync(r)) return rc;
+    fc::ChainScalars s;
+    HIP_TRY(hipMemcpy(&s, r->d_sc + chain, sizeof s, hipMemcpyDeviceToHost));
+    const int64_t n = std::min<int64_t>({s.trace_len, r->p.trace_cap, cap});
+    static_assert(sizeof(fc_recom_record) == sizeof(fc_record), "trace slots are shared");
+    HIP_TRY(hipMemcpy(out, (const fc_recom_record *)r->d_trace + (size_t)chain * r->p.trace_cap,
+                      (size_t)n * sizeof(fc_recom_record), hipMemcpyDeviceToHost));
     *len = s.trace_len;
     return FC_OK;
 }

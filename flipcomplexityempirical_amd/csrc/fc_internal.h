@@ -132,6 +132,27 @@ struct KParams {
 //        9 one-event classify, 10 one-event apply, 11 segment-parallel, 12 segments
 constexpr int kProfSlots = 16;
 
+// ReCom kernel parameters (fc_recom.hip).
+struct RecomParams {
+    const void *graph;             // NodeRec<RMAX>[n]
+    const int32_t *ring_eid;       // [n * RMAX] canonical edge id of each ring neighbour slot
+    const int32_t *eu, *ev;        // [n_edges] canonical edge list
+    int32_t n, n_edges, n_chains, chain_lds_bytes;
+    uint32_t chain_id_offset, seed_lo, seed_hi;
+    int32_t pop_lo, pop_hi;
+    double pop_target, epsilon;
+    int32_t node_repeats, max_attempts;
+    int64_t n_steps, max_draws;
+    int8_t *assign;
+    ChainScalars *sc;              // attempts in bfs_calls, spanning trees in bfs_levels
+    const uint64_t *accept_thresh; // [2 n_edges + 1]: U53 thresholds of base ** (cut - cut')
+    fc_recom_record *trace;
+    int32_t trace_chains;
+    int64_t trace_cap;
+};
+inline int recom_lds_bytes(int n) { return 19 * ((n + 15) & ~15) + 16; }
+int launch_recom(const RecomParams &p, int ring_max, void *stream, char *name, size_t name_cap);
+
 // Launch wrappers (fc_kernels.hip).  Return a hipError_t as int.
 // `name` (may be null) receives the launched instance, spelled as rocprofv3 reports it.
 int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap);  // k > 2

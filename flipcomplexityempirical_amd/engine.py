@@ -22,6 +22,8 @@ _P = ctypes.POINTER
 STAT_FIELDS = [f for f, _ in _lib.ChainStats._fields_]
 RECORD_DTYPE = np.dtype([("draw", "<i8"), ("v", "<i4"), ("flags", "<i4"), ("cut", "<i4"),
                          ("nb", "<i4"), ("wait", "<i8")])
+RECOM_RECORD_DTYPE = np.dtype([("draw", "<i8"), ("edge", "<i4"), ("root", "<i4"), ("child", "<i4"),
+                               ("attempts", "<i4"), ("flags", "<i4"), ("cut", "<i4")])
 EVENT_DTYPE = np.dtype([("t", "<i8"), ("v", "<u2"), ("cut", "<u2"), ("nb", "<u2"), ("target", "u1"),
                         ("reserved", "u1")])
 
@@ -110,6 +112,11 @@ class RunConfig:
     con_accept: int = 0      # FC_CON_* tested by the accept callable
     beta: float = 0.0        # FC_ACCEPT_ANNEAL exponent factor
     frozen: Sequence[int] = ()  # FC_CON_FIXED: endpoints of the pinned edges
+    # FC_PROPOSE_RECOM: recom(pop_target, epsilon, node_repeats) (grid_chain_sec11.py:328-335)
+    recom_pop_target: float = 0.0
+    recom_epsilon: float = 0.05
+    recom_node_repeats: int = 1
+    recom_max_attempts: int = 0
 
 
 class FlipRun:
@@ -147,6 +154,10 @@ class FlipRun:
         self._frozen = np.ascontiguousarray(list(cfg.frozen), dtype=np.int32)
         prm.frozen = _p(self._frozen, ctypes.c_int32)
         prm.n_frozen = int(self._frozen.size)
+        prm.recom_pop_target = float(cfg.recom_pop_target)
+        prm.recom_epsilon = float(cfg.recom_epsilon)
+        prm.recom_node_repeats = int(cfg.recom_node_repeats)
+        prm.recom_max_attempts = int(cfg.recom_max_attempts)
         h = ctypes.c_void_p()
         check(L.fc_run_create(graph.handle, ctypes.byref(prm), self.n_chains, _p(self._init, ctypes.c_int8),
                               _p(self._bases, ctypes.c_double), ctypes.byref(h)), "fc_run_create")
@@ -208,6 +219,18 @@ class FlipRun:
         n = ctypes.c_int64(0)
         check(_lib.load().fc_run_read_trace(self.handle, chain, ctypes.cast(out.ctypes.data, _P(_lib.Record)),
                                             cap, ctypes.byref(n)), "fc_run_read_trace")
+        if n.value > cap:
+            raise OverflowError(f"trace capacity {cap} exceeded ({n.value} records)")
+        return out[:n.value]
+
+    def recom_trace(self, chain: int = 0) -> np.ndarray:
+        """Per-proposal records of a traced ReCom chain (``fc_recom_record``)."""
+        cap = self.cfg.trace_cap
+        out = np.zeros(cap, dtype=RECOM_RECORD_DTYPE)
+        n = ctypes.c_int64(0)
+        check(_lib.load().fc_run_read_recom_trace(self.handle, chain,
+                                                  ctypes.cast(out.ctypes.data, _P(_lib.RecomRecord)), cap,
+                                                  ctypes.byref(n)), "fc_run_read_recom_trace")
         if n.value > cap:
             raise OverflowError(f"trace capacity {cap} exceeded ({n.value} records)")
         return out[:n.value]

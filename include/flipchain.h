@@ -43,6 +43,8 @@ extern "C" {
 /* fc_params.proposal */
 #define FC_PROPOSE_BI_SIGN 0     /* slow_reversible_propose_bi, grid_chain_sec11.py:132-145 */
 #define FC_PROPOSE_PAIR 1        /* slow_reversible_propose,    grid_chain_sec11.py:117-130 */
+#define FC_PROPOSE_RECOM 2       /* recom tree proposal built at grid_chain_sec11.py:328-335:
+                                    spanning-tree bipartition of two merged districts       */
 
 /* fc_params.diag_mask: per-yield driver diagnostics kept on the device
  * (grid_chain_sec11.py:350-419).  The streaming sums are always kept.                    */
@@ -116,6 +118,12 @@ typedef struct fc_params {
     double beta;               /* FC_ACCEPT_ANNEAL exponent factor (the reference: 5)       */
     const int32_t *frozen;     /* FC_CON_FIXED: [n_frozen] endpoints of the pinned edges    */
     int32_t n_frozen;
+    /* FC_PROPOSE_RECOM: recom(pop_target, epsilon, node_repeats) [gc-0.2]; the Validator is
+       the population bound, acceptance is cut_accept with `base` (1: always_accept)        */
+    double recom_pop_target;
+    double recom_epsilon;
+    int32_t recom_node_repeats;  /* roots tried per spanning tree (<= 0: 1)                */
+    int32_t recom_max_attempts;  /* roots tried per proposal before giving up (<= 0: 10000) */
 } fc_params;
 
 /* Per-chain statistics.  "Yields" are the states a `for part in exp_chain` loop sees:
@@ -167,6 +175,17 @@ typedef struct fc_record {
     int64_t wait;         /* geometric wait of the yielded state (valid proposals)        */
 } fc_record;
 
+/* One ReCom proposal (trace mode, FC_PROPOSE_RECOM), identical in layout to the oracle's. */
+typedef struct fc_recom_record {
+    int64_t draw;
+    int32_t edge;         /* cut edge chosen (canonical edge id): its two districts merge   */
+    int32_t root;         /* spanning-tree root of the successful attempt                   */
+    int32_t child;        /* the cut's child: subtree(child) -> district of edge's first end */
+    int32_t attempts;     /* roots tried                                                     */
+    int32_t flags;        /* 1 valid, 2 accepted, 8 invalid: population                      */
+    int32_t cut;          /* |cut edges| after the proposal                                  */
+} fc_recom_record;
+
 /* ---- graph: replaces gerrychain Graph + the networkx lattice (:186-260) ------------ */
 /* CSR adjacency (symmetric, no self loops), node populations (Tally('population'),
  * :299), optional planar positions [2n] from which the per-node link rings and the
@@ -205,6 +224,8 @@ int fc_run_read_state(fc_run *r, int8_t *assign_out);
 /* District populations [c * k] (Tally('population'), :299). */
 int fc_run_read_pops(fc_run *r, int64_t *pops_out);
 int fc_run_read_trace(fc_run *r, int32_t chain, fc_record *out, int64_t cap, int64_t *len);
+/* ReCom runs: the per-proposal records of a traced chain (*len may exceed cap). */
+int fc_run_read_recom_trace(fc_run *r, int32_t chain, fc_recom_record *out, int64_t cap, int64_t *len);
 /* Restart every traced chain's record buffer at 0 (chunked per-step iteration). */
 int fc_run_trace_reset(fc_run *r);
 int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist);      /* [c*(E+1)], [c*(n+1)] */

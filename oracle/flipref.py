@@ -132,7 +132,8 @@ class FrOutputs(ctypes.Structure):
 
 def build_lib(force: bool = False) -> str:
     if force or not os.path.exists(LIB_PATH) or \
-            os.path.getmtime(LIB_PATH) < max(os.path.getmtime(os.path.join(HERE, f)) for f in ("flipref.c", "flipref.h")):
+            os.path.getmtime(LIB_PATH) < max(os.path.getmtime(os.path.join(HERE, f))
+                                             for f in ("flipref.c", "flipref.h", "recomref.c", "recomref.h")):
         subprocess.run(["make", "-C", HERE, "-s"], check=True)
     return LIB_PATH
 
@@ -580,3 +581,56 @@ def cut_edge_labels(spec, assign: np.ndarray) -> set:
     e = spec.edges()
     m = assign[e[:, 0]] != assign[e[:, 1]]
     return {tuple(sorted((spec.nodes[u], spec.nodes[v]))) for u, v in e[m]}
+
+
+# --------------------------------------------------------------------------------------
+# ReCom (oracle/recomref.c): gerrychain 0.2 recom + bipartition_tree restated
+# (grid_chain_sec11.py:328-335 builds it), checker of the HIP ReCom kernel.
+# --------------------------------------------------------------------------------------
+class RrParams(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("row_ptr", _P(ctypes.c_int32)), ("col_idx", _P(ctypes.c_int32)),
+                ("pop", _P(ctypes.c_int32)), ("k", ctypes.c_int32), ("pop_target", ctypes.c_double),
+                ("epsilon", ctypes.c_double), ("node_repeats", ctypes.c_int32), ("max_attempts", ctypes.c_int32),
+                ("pop_lo", ctypes.c_int64), ("pop_hi", ctypes.c_int64), ("base", ctypes.c_double),
+                ("seed", ctypes.c_uint64), ("chain_id", ctypes.c_uint32), ("n_steps", ctypes.c_int64),
+                ("max_draws", ctypes.c_int64)]
+
+
+class RrStats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int64) for f in ("steps", "proposals", "accepted", "inv_pop", "attempts", "trees",
+                                             "sum_cut", "sum_nb")] + \
+               [(f, ctypes.c_int32) for f in ("cut", "nb", "stuck", "pad")]
+
+
+RR_RECORD_DTYPE = np.dtype([("draw", "<i8"), ("edge", "<i4"), ("root", "<i4"), ("child", "<i4"),
+                            ("attempts", "<i4"), ("flags", "<i4"), ("cut", "<i4")])
+
+
+def recom_run(spec, init_assign: np.ndarray, *, k: int, pop_target: float, epsilon: float, pop_lo: int,
+              pop_hi: int, seed: int, chain_id: int, n_steps: int, node_repeats: int = 1, base: float = 1.0,
+              max_attempts: int = 100000, max_draws: int = 0, trace_cap: int = 0) -> Dict:
+    """One ReCom chain on the CPU (``rr_run``): stats, final assignment, per-proposal trace."""
+    L = ctypes.CDLL(build_lib())
+    L.rr_run.argtypes = [ctypes.POINTER(RrParams), _P(ctypes.c_int8), ctypes.POINTER(RrStats), _P(ctypes.c_int8),
+                         ctypes.c_void_p, ctypes.c_int64, _P(ctypes.c_int64)]
+    row_ptr = np.ascontiguousarray(spec.row_ptr, dtype=np.int32)
+    col_idx = np.ascontiguousarray(spec.col_idx, dtype=np.int32)
+    pop = np.ascontiguousarray(spec.pop, dtype=np.int32)
+    init = np.ascontiguousarray(init_assign, dtype=np.int8)
+    p = RrParams(n=spec.n, row_ptr=_ptr(row_ptr, ctypes.c_int32), col_idx=_ptr(col_idx, ctypes.c_int32),
+                 pop=_ptr(pop, ctypes.c_int32), k=k, pop_target=float(pop_target), epsilon=float(epsilon),
+                 node_repeats=int(node_repeats), max_attempts=int(max_attempts), pop_lo=int(pop_lo),
+                 pop_hi=int(pop_hi), base=float(base), seed=int(seed), chain_id=int(chain_id),
+                 n_steps=int(n_steps), max_draws=int(max_draws))
+    st = RrStats()
+    final = np.zeros(spec.n, dtype=np.int8)
+    trace = np.zeros(max(trace_cap, 1), dtype=RR_RECORD_DTYPE)
+    tl = ctypes.c_int64(0)
+    rc = L.rr_run(ctypes.byref(p), _ptr(init, ctypes.c_int8), ctypes.byref(st), _ptr(final, ctypes.c_int8),
+                  ctypes.c_void_p(trace.ctypes.data), int(trace_cap), ctypes.byref(tl))
+    if rc == -1:
+        raise ValueError("The given initial_state is not valid according is_valid.")
+    if rc == -2:
+        raise RuntimeError("rr_run: bad arguments")
+    return {"rc": rc, "stats": {f: int(getattr(st, f)) for f, _ in RrStats._fields_}, "final": final,
+            "trace": trace[:tl.value].copy()}

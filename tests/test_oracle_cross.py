@@ -161,3 +161,20 @@ def test_oracle_variants_respect_their_constraints(cref, sec11):
     s2 = r2["stats"]
     assert s2["inv_contig"] == 0 and s2["inv_pop"] == 0 and s2["steps"] == s2["proposals"] == 5000
     assert 0 < s2["accepted"] < 5000
+
+
+def test_recom_oracle_keeps_plans_valid(cref, sec11):
+    """The ReCom restatement moves whole subtrees: every state it yields has contiguous
+    districts inside the population bound, and it accepts every valid step at base 1."""
+    from flipcomplexityempirical_amd import graphs as G
+    from oracle.flipref import recom_run
+    a0 = sec11.assignment_array(G.sec11_plan(2, sec11.nodes), [-1, 1])
+    _, (lo, hi) = G.population_bounds(sec11.n, 2, 0.1)
+    r = recom_run(sec11, a0, k=2, pop_target=sec11.n / 2, epsilon=0.05, pop_lo=lo, pop_hi=hi, seed=4, chain_id=1,
+                  n_steps=50, trace_cap=200)
+    s = r["stats"]
+    assert s["steps"] == 50 and s["accepted"] == 50 and s["trees"] >= 50
+    assert cref.districts_contiguous(sec11, r["final"], 2)
+    cut, nb, pops = G.cut_and_boundary(sec11, r["final"])
+    assert (cut, nb) == (s["cut"], s["nb"]) and lo <= pops.min() and pops.max() <= hi
+    assert np.all(np.abs(np.array([pops[0], pops[1]]) - sec11.n / 2) < 0.05 * sec11.n / 2)

@@ -1,0 +1,71 @@
+"""GPU parity of the ReCom tree proposal against the C oracle.
+
+The reference builds ``tree_proposal = partial(recom, pop_col="population",
+pop_target=ideal_population, epsilon=0.05, node_repeats=1)`` (grid_chain_sec11.py:328-335)
+beside its flip chain.  The device kernel (``fc_recom.hip``: Boruvka maximum spanning tree,
+level-synchronous rooting, subtree populations) and ``oracle/recomref.c`` (Kruskal, DFS)
+consume the same canonical stream (recomref.h), so the per-proposal records -- cut edge,
+root, cut child, roots tried, validity, acceptance, |cut| -- final states and statistics
+must agree bit for bit.
+"""
+import numpy as np
+import pytest
+
+from flipcomplexityempirical_amd import _lib
+from flipcomplexityempirical_amd import graphs as G
+from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+from oracle.flipref import recom_run
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    # name: (graph, k, plan, pct, epsilon, node_repeats, base, steps)
+    "sec11 k=2": ("sec11", 2, "sec11:0", 0.1, 0.05, 1, 1.0, 60),
+    "sec11 k=4 cut_accept": ("sec11", 4, "quadrant", 0.1, 0.05, 1, 1.5, 80),
+    "frank k=2 node_repeats=2": ("frank", 2, "frank:1", 0.1, 0.05, 2, 1.0, 60),
+}
+
+
+def _setup(case):
+    gname, k, plan, pct, eps, reps, base, steps = CASES[case]
+    spec = G.sec11_graph() if gname == "sec11" else G.frank_graph()
+    labels = [-1, 1] if k == 2 else list(range(k))
+    if plan.startswith("sec11"):
+        a0 = spec.assignment_array(G.sec11_plan(int(plan[-1]), spec.nodes), labels)
+    elif plan.startswith("frank"):
+        a0 = spec.assignment_array(G.frank_plan(int(plan[-1]), spec.nodes), labels)
+    else:
+        a0 = spec.assignment_array(G.quadrant_plan(spec.nodes), labels)
+    total = int(spec.pop.sum())
+    _, (lo, hi) = G.population_bounds(total, k, pct)
+    return spec, k, labels, a0, total / k, lo, hi, eps, reps, base, steps
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_recom_matches_oracle(gpu, case):
+    spec, k, labels, a0, ideal, lo, hi, eps, reps, base, steps = _setup(case)
+    n_chains = 4
+    cfg = RunConfig(k=k, labels=tuple(labels), proposal=_lib.FC_PROPOSE_RECOM, seed=99, pop_lo=lo, pop_hi=hi,
+                    base=base, recom_pop_target=ideal, recom_epsilon=eps, recom_node_repeats=reps,
+                    trace_chains=n_chains, trace_cap=4 * steps, diag_mask=0)
+    run = FlipRun(FlipGraph(spec), np.stack([a0] * n_chains), cfg)
+    run.steps(steps // 2)
+    run.steps(steps - steps // 2)  # across launches
+    st, fin = run.stats(), run.state()
+    assert run.kernel_name().startswith("fc::recom_kernel<")
+    for c in range(n_chains):
+        ref = recom_run(spec, a0, k=k, pop_target=ideal, epsilon=eps, pop_lo=lo, pop_hi=hi, seed=99, chain_id=c,
+                        n_steps=steps, node_repeats=reps, base=base, trace_cap=4 * steps)
+        tr, rt = run.recom_trace(c), ref["trace"]
+        assert len(tr) == len(rt), (case, c)
+        for f in ("draw", "edge", "root", "child", "attempts", "flags", "cut"):
+            assert np.array_equal(tr[f], rt[f]), (case, c, f)
+        assert np.array_equal(fin[c], ref["final"]), (case, c)
+        rs = ref["stats"]
+        for kd, kr in (("steps", "steps"), ("proposals", "proposals"), ("accepted", "accepted"),
+                       ("inv_pop", "inv_pop"), ("sum_cut", "sum_cut"), ("sum_nb", "sum_nb"), ("cut", "cut"),
+                       ("nb", "nb"), ("bfs_calls", "attempts"), ("bfs_levels", "trees")):
+            assert int(st[kd][c]) == int(rs[kr]), (case, c, kd)
+        # every state is a plan of k contiguous districts inside the bounds
+        cut, nb, pops = G.cut_and_boundary(spec, fin[c])
+        assert cut == int(st["cut"][c]) and pops.min() >= lo and pops.max() <= hi
