@@ -251,6 +251,38 @@ class AnnealingCutAcceptBackwards:
         return random.random() < bound
 
 
+def recom(partition, pop_col, pop_target, epsilon, node_repeats=1):
+    """gerrychain 0.2 ``recom`` [gc-0.2], the tree proposal the reference builds at
+    ``grid_chain_sec11.py:328-335`` (host use; the device runs it from the compiled chain):
+    merge the two districts of a random cut edge, draw a random spanning tree (maximum
+    spanning tree of uniform edge weights), and split it at a random edge whose subtree
+    population is within ``epsilon`` of ``pop_target`` (new root / tree while there is none)."""
+    import networkx as nx
+    edge = random.choice(tuple(partition["cut_edges"]))
+    parts = (partition.assignment[edge[0]], partition.assignment[edge[1]])
+    nodes = [n for n in partition.graph.nodes if partition.assignment[n] in parts]
+    sub = partition.graph.subgraph(nodes)
+    pops = {n: sub.nodes[n][pop_col] for n in sub.nodes}
+    while True:
+        h = nx.Graph()
+        h.add_nodes_from(sub.nodes)
+        h.add_weighted_edges_from((u, v, random.random()) for u, v in sub.edges)
+        tree = nx.maximum_spanning_tree(h, algorithm="kruskal")
+        for _ in range(node_repeats):
+            root = random.choice([x for x in tree if tree.degree(x) > 1])
+            pred = dict(nx.bfs_predecessors(tree, root))
+            order = [root] + [v for _, v in nx.bfs_edges(tree, root)]
+            sub_pop = dict(pops)
+            for x in reversed(order[1:]):
+                sub_pop[pred[x]] += sub_pop[x]
+            cuts = [x for x in order[1:] if abs(sub_pop[x] - pop_target) < epsilon * pop_target]
+            if cuts:
+                child = random.choice(cuts)
+                below = set(nx.dfs_preorder_nodes(tree.subgraph(set(tree) - {pred[child]}), child))
+                flips = {n: (parts[0] if n in below else parts[1]) for n in nodes}
+                return partition.flip(flips)
+
+
 uniform_accept = UniformAccept()
 annealing_cut_accept_backwards = AnnealingCutAcceptBackwards()
 
@@ -332,6 +364,8 @@ class ChainSpec:
     pinned: List[tuple] = field(default_factory=list)
     frozen: List[int] = field(default_factory=list)
     boundary_nodes: Optional[List[Hashable]] = None
+    proposal: int = 0               # FC_PROPOSE_*
+    recom: Optional[Dict[str, Any]] = None  # pop_target, epsilon, node_repeats
 
 
 def _bounds_of(b) -> tuple:
@@ -341,9 +375,16 @@ def _bounds_of(b) -> tuple:
 
 def compile_chain(proposal, constraints, accept, initial_state: Partition) -> ChainSpec:
     """Map the reference's callables onto the device chain (NotImplementedError otherwise)."""
-    if _name(proposal) != "slow_reversible_propose_bi":
+    import functools
+    recom_kw = None
+    if isinstance(proposal, functools.partial) and getattr(proposal.func, "__name__", "") == "recom":
+        kw = dict(proposal.keywords)
+        recom_kw = {"pop_col": kw.get("pop_col", "population"), "pop_target": float(kw["pop_target"]),
+                    "epsilon": float(kw["epsilon"]), "node_repeats": int(kw.get("node_repeats", 1))}
+    elif _name(proposal) != "slow_reversible_propose_bi":
         raise NotImplementedError(f"proposal {_name(proposal)!r}: the device implements "
-                                  "slow_reversible_propose_bi (grid_chain_sec11.py:132-145)")
+                                  "slow_reversible_propose_bi (grid_chain_sec11.py:132-145) and "
+                                  "partial(recom, ...) (:328-335)")
     cons = constraints.constraints if isinstance(constraints, Validator) else (
         list(constraints) if isinstance(constraints, (list, tuple)) else [constraints])
     contig_idx, bounds, pop_key = None, None, "population"
@@ -387,7 +428,7 @@ def compile_chain(proposal, constraints, accept, initial_state: Partition) -> Ch
                                   "uniform_accept / annealing_cut_accept_backwards")
     if con_valid == 0:
         con_valid = _lib.FC_CON_EMPTY  # Validator([]): nothing re-draws
-    if not ((con_valid | con_accept) & _lib.FC_CON_CONTIG):
+    if recom_kw is None and not ((con_valid | con_accept) & _lib.FC_CON_CONTIG):
         raise NotImplementedError("the device chain keeps districts connected: single_flip_contiguous must be "
                                   "in the Validator or the accept callable")
     # one population bound on the device: the Validator's, the accept's, or both equal
@@ -399,7 +440,13 @@ def compile_chain(proposal, constraints, accept, initial_state: Partition) -> Ch
         raise NotImplementedError("the Validator's and the accept callable's population bounds differ")
     g = initial_state.graph
     labels = sorted(set(initial_state.assignment.values()))
-    if len(labels) != 2 or sorted(labels) != [-1, 1]:
+    if recom_kw is not None:
+        if con_valid & ~(_lib.FC_CON_POP | _lib.FC_CON_CONTIG) or acc_kind != _lib.FC_ACCEPT_CUT:
+            raise NotImplementedError("recom runs with the population Validator and cut_accept / always_accept")
+        if recom_kw["pop_col"] != pop_key and bounds is not None:
+            raise NotImplementedError("recom pop_col and the population bound must use the same column")
+        pop_key = recom_kw["pop_col"]
+    elif len(labels) != 2 or sorted(labels) != [-1, 1]:
         raise NotImplementedError("slow_reversible_propose_bi flips -1 <-> 1: the plan must use labels -1 / 1")
     for n in g.nodes:
         g.nodes[n].setdefault(pop_key, 1)
@@ -422,7 +469,9 @@ def compile_chain(proposal, constraints, accept, initial_state: Partition) -> Ch
     return ChainSpec(spec=spec, labels=labels, init=init, base=base, pop_lo=lo, pop_hi=hi,
                      pop_bounds_float=(lo_f, hi_f), contig_first=contig_first, pop_key=pop_key,
                      accept=acc_kind, con_valid=con_valid, con_accept=con_accept, beta=beta, pinned=pinned,
-                     frozen=frozen, boundary_nodes=bnodes)
+                     frozen=frozen, boundary_nodes=bnodes,
+                     proposal=_lib.FC_PROPOSE_RECOM if recom_kw is not None else _lib.FC_PROPOSE_BI_SIGN,
+                     recom=recom_kw)
 
 
 def check_device_constraints(cs: ChainSpec, graph) -> None:
@@ -537,6 +586,14 @@ class MarkovChain:
         from .engine import FlipGraph, FlipRun, RunConfig
         if self._graph is None:
             self._graph = FlipGraph(self.cspec.spec)
+        cs = self.cspec
+        if cs.proposal == _lib.FC_PROPOSE_RECOM:
+            cfg = RunConfig(k=len(cs.labels), labels=tuple(cs.labels), proposal=cs.proposal, seed=self.seed,
+                            chain_id_offset=self.chain_id, pop_lo=cs.pop_lo, pop_hi=cs.pop_hi, base=cs.base,
+                            device=self.device, diag_mask=0, trace_chains=1 if trace else 0,
+                            trace_cap=self.chunk + 16 if trace else 0, recom_pop_target=cs.recom["pop_target"],
+                            recom_epsilon=cs.recom["epsilon"], recom_node_repeats=cs.recom["node_repeats"])
+            return FlipRun(self._graph, cs.init[None, :], cfg)
         cfg = RunConfig(seed=self.seed, chain_id_offset=self.chain_id, pop_lo=self.cspec.pop_lo,
                         pop_hi=self.cspec.pop_hi, base=self.cspec.base, device=self.device, diag_mask=diag,
                         trace_chains=1 if trace else 0, trace_cap=64 * self.chunk + 4096 if trace else 0,
@@ -547,6 +604,9 @@ class MarkovChain:
 
     # ---- per-step iteration (debugging path) -------------------------------------------
     def __iter__(self):
+        if self.cspec.proposal == _lib.FC_PROPOSE_RECOM:
+            yield from self._iter_recom()
+            return
         run = self._make_run(trace=True, diag=_lib.FC_DIAG_WAIT)
         sp, lab = self.cspec.spec, self.cspec.labels
         a = self.cspec.init.copy()
@@ -570,6 +630,44 @@ class MarkovChain:
                 yield view
         run.close()
 
+    def _run_recom(self) -> "ChainResult":
+        """ReCom on the device: the driver's sums (|cut|, |B| over yields), acceptance
+        counts, spanning trees (``stats["bfs_levels"]``) and roots tried (``stats["bfs_calls"]``)."""
+        if self._graph is None:
+            from .engine import FlipGraph
+            self._graph = FlipGraph(self.cspec.spec)
+        run = self._make_run(trace=False, diag=0)
+        if self.total_steps > 1:
+            run.steps(self.total_steps - 1)
+        res = _recom_result(self, run)
+        run.close()
+        return res
+
+    def _iter_recom(self):
+        """ReCom yields, one device step per yield (debugging path): the state is read back
+        after every step; ``flips`` holds the nodes the last accepted proposal moved."""
+        if self._graph is None:
+            from .engine import FlipGraph
+            self._graph = FlipGraph(self.cspec.spec)
+        run = self._make_run(trace=False, diag=0)
+        sp, lab = self.cspec.spec, self.cspec.labels
+        a = self.cspec.init.copy()
+        st = run.stats()
+        view = StateView(self, a.copy(), None, 0, int(st["cut"][0]), int(st["nb"][0]), 0)
+        yield view
+        for t in range(1, self.total_steps):
+            acc0 = int(st["accepted"][0])
+            run.steps(1)
+            st = run.stats()
+            if int(st["accepted"][0]) > acc0:
+                b = run.state()[0]
+                moved = np.nonzero(b != a)[0]
+                a = b
+                view = StateView(self, a.copy(), {sp.nodes[i]: lab[a[i]] for i in moved}, 0, int(st["cut"][0]),
+                                 int(st["nb"][0]), t)
+            yield view
+        run.close()
+
     # ---- fast path -------------------------------------------------------------------
     def run(self, series: bool = True, frame: Optional[str] = "auto") -> "ChainResult":
         """All ``total_steps`` yields on the device; the reference driver's outputs
@@ -579,6 +677,8 @@ class MarkovChain:
         device event log; ``frame`` ("sec11", "frank", None or "auto": from the
         ``slope`` updater and the node labels) adds the ``slopes`` / ``angles`` lists
         (``:371-394``) computed by ``fc_run_frame_series``."""
+        if self.cspec.proposal == _lib.FC_PROPOSE_RECOM:
+            return self._run_recom()
         diag = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
         if frame == "auto":
             frame = None
@@ -600,6 +700,18 @@ class MarkovChain:
                 res.angles = run.yield_series(fs["angle"][0], 0)
         run.close()
         return res
+
+
+def _recom_result(chain: "MarkovChain", run) -> "ChainResult":
+    sp, lab = chain.cspec.spec, chain.cspec.labels
+    st = run.stats()
+    fin = run.state()[0]
+    return ChainResult(
+        steps=int(st["steps"][0]), proposals=int(st["proposals"][0]), accepted=int(st["accepted"][0]),
+        waits_sum=0, rce_sum=int(st["sum_cut"][0]), rbn_sum=int(st["sum_nb"][0]),
+        cut_hist=np.zeros(0, dtype=np.int64), nb_hist=np.zeros(0, dtype=np.int64), cut_times={}, num_flips={},
+        part_sum={}, last_flipped={}, lognum_flips={}, final_assignment={sp.nodes[i]: lab[fin[i]] for i in range(sp.n)},
+        stats={k: int(v[0]) for k, v in st.items()})
 
 
 @dataclass

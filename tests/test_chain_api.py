@@ -113,3 +113,28 @@ def test_variant_callables_compile(sec11):
                        accept=fc.cut_accept, initial_state=part2, total_steps=10)
     with pytest.raises(NotImplementedError):  # contiguity nowhere
         fc.compile_chain(fc.slow_reversible_propose_bi, fc.Validator([pb]), fc.cut_accept, part)
+
+
+def test_recom_partial_compiles_and_host_recom_is_valid():
+    """``partial(recom, pop_col="population", pop_target=ideal, epsilon=0.05, node_repeats=1)``
+    (grid_chain_sec11.py:328-335) compiles to FC_PROPOSE_RECOM; the host restatement of
+    recom returns a balanced, contiguous two-district plan."""
+    import functools
+    import random as _random
+    from flipcomplexityempirical_amd import _lib
+    from flipcomplexityempirical_amd import chain as fc
+    from flipcomplexityempirical_amd import graphs as G
+    graph = G.sec11_nx()
+    part = fc.Partition(graph, assignment=G.sec11_plan(0, sorted(graph.nodes())),
+                        updaters={"population": fc.Tally("population"), "cut_edges": fc.cut_edges})
+    ideal = sum(part["population"].values()) / len(part)
+    tree_proposal = functools.partial(fc.recom, pop_col="population", pop_target=ideal, epsilon=0.05, node_repeats=1)
+    pb = fc.within_percent_of_ideal_population(part, 0.1)
+    cs = fc.compile_chain(tree_proposal, fc.Validator([pb]), fc.always_accept, part)
+    assert cs.proposal == _lib.FC_PROPOSE_RECOM and cs.recom == {"pop_col": "population", "pop_target": ideal,
+                                                                 "epsilon": 0.05, "node_repeats": 1}
+    _random.seed(3)
+    nxt = tree_proposal(part)
+    assert fc.contiguous(nxt)
+    pops = list(nxt["population"].values())
+    assert all(abs(p_ - ideal) < 0.05 * ideal for p_ in pops)

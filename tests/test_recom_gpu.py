@@ -69,3 +69,29 @@ def test_recom_matches_oracle(gpu, case):
         # every state is a plan of k contiguous districts inside the bounds
         cut, nb, pops = G.cut_and_boundary(spec, fin[c])
         assert cut == int(st["cut"][c]) and pops.min() >= lo and pops.max() <= hi
+
+
+def test_markov_chain_recom_matches_oracle(gpu):
+    """The reference-shaped tree_proposal chain: fast path and per-step iterator agree with
+    each other and with the oracle."""
+    import functools
+    from flipcomplexityempirical_amd import chain as fc
+    graph = G.sec11_nx()
+    part = fc.Partition(graph, assignment=G.sec11_plan(1, sorted(graph.nodes())),
+                        updaters={"population": fc.Tally("population"), "cut_edges": fc.cut_edges})
+    ideal = sum(part["population"].values()) / len(part)
+    tree_proposal = functools.partial(fc.recom, pop_col="population", pop_target=ideal, epsilon=0.05, node_repeats=1)
+    pb = fc.within_percent_of_ideal_population(part, 0.1)
+    chain = fc.MarkovChain(tree_proposal, fc.Validator([pb]), accept=fc.always_accept, initial_state=part,
+                           total_steps=41, seed=17, chain_id=2)
+    res = chain.run()
+    cs = chain.cspec
+    ref = recom_run(cs.spec, cs.init, k=2, pop_target=ideal, epsilon=0.05, pop_lo=cs.pop_lo, pop_hi=cs.pop_hi,
+                    seed=17, chain_id=2, n_steps=40)
+    assert res.steps == 40 and res.rce_sum == ref["stats"]["sum_cut"] and res.accepted == ref["stats"]["accepted"]
+    views = list(chain)
+    assert len(views) == 41
+    last = views[-1]
+    for nd in graph.nodes():
+        assert last.assignment[nd] == res.final_assignment[nd]
+    assert sum(len(v["cut_edges"]) for v in views) == res.rce_sum
