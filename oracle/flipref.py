@@ -467,6 +467,54 @@ class GcFaithfulChain:
         return np.asarray([lut[self.state.assignment[nd]] for nd in self.spec.nodes], dtype=np.int8)
 
 
+class NativeRngChain(GcFaithfulChain):
+    """The reference's flip step under its own (native) random streams, for the
+    distributional checks: ``random.choice(list(partition["b_nodes"]))`` (:143),
+    ``random.random()`` in cut_accept (:179), ``np.random.geometric`` in geom_wait (:148),
+    and the ``random.choice`` that gerrychain's single_flip_contiguous makes among the old
+    neighbours [gc-0.2] -- CPython's Mersenne Twister and numpy's legacy RandomState,
+    seeded per chain instead of globally."""
+
+    def __init__(self, spec, plan: Dict, *, base: float, pop_bounds, seed: int,
+                 log1mp: Optional[np.ndarray] = None):
+        import random as _random
+        self.rng = _random.Random(seed)
+        self.nprng = np.random.RandomState(seed & 0xFFFFFFFF)
+        super().__init__(spec, plan, base=base, pop_bounds=pop_bounds, seed=seed, chain_id=0, log1mp=log1mp)
+
+    def _geom(self, d, purpose):
+        if self.log1mp is None:
+            return 0
+        s = self.state
+        p = len(list(s["b_nodes"])) / (len(self.g.nodes) ** len(self.labels) - 1)  # :148
+        return int(self.nprng.geometric(p, 1)[0]) - 1
+
+    def step(self):
+        while True:
+            s = self.state
+            node = self.rng.choice(list(s["b_nodes"]))  # :143
+            self.stats["draws"] += 1
+            self.stats["proposals"] += 1
+            target = -1 * s.assignment[node]  # :145
+            proposal = s.flip({node: target})
+            s.parent = None
+            old_nbrs = [nd for nd in self.g.neighbors(node) if proposal.assignment[nd] == s.assignment[node]]
+            if old_nbrs:
+                self.rng.choice(old_nbrs)  # single_flip_contiguous's start node [gc-0.2]
+            bad = self._valid(proposal)
+            if bad:
+                self.stats["inv_contig" if bad == FLAG_INV_CONTIG else "inv_pop"] += 1
+                continue
+            self.stats["steps"] += 1
+            bound = self.base ** (-len(proposal["cut_edges"]) + len(s["cut_edges"]))  # :175
+            if self.rng.random() < bound:  # :179
+                self.state = proposal
+                self.stats["accepted"] += 1
+                self.wait = self._geom(0, 1)
+            self._yield()
+            return self.state
+
+
 # --------------------------------------------------------------------------------------
 # Series diagnostics restated from a proposal trace (checker for FC_DIAG_SERIES).
 # The reference driver keeps the per-yield lists rce / rbn (grid_chain_sec11.py:367-369);
