@@ -2,12 +2,15 @@
 and district-shape statistics under native RNG").
 
 The reference's flip step driven by CPython's Mersenne Twister and numpy's legacy geometric
-(oracle.flipref.NativeRngChain; fixture tests/golden/native_rng_c1.npz, made by
-tests/golden/make_native.py) against the canonical Philox stream of the C oracle, on
-BASELINE config C1 (10x10 grid, k = 2, plan x[0] >= 5, pop tolerance 0.1) at bases 1 and mu,
-2000 steps: two-sample KS tests on the end state's |cut edges|, |b_nodes| and district
-population, the time-averaged |cut| and |B| of each chain, and the geometric wait.  The
-device is held to the same fixture in tests/test_distribution_gpu.py.
+(oracle.flipref.NativeRngChain; fixtures tests/golden/native_rng_{c1,sec11}.npz, made by
+tests/golden/make_native.py) against the canonical Philox stream of the C oracle:
+  c1:    BASELINE config C1 (10x10 grid, k = 2, plan x[0] >= 5, pop tolerance 0.1),
+         bases 1 and mu, 2000 steps;
+  sec11: the headline lattice (grid_chain_sec11.py:186-260), alignment-2 plan, pop
+         tolerance 0.1, bases 0.8 and mu, 1000 steps.
+Two-sample KS tests on the end state's |cut edges|, |b_nodes| and district population, each
+chain's time-averaged |cut| and |B|, and the geometric wait of the end state.  The device is
+held to the same fixtures in tests/test_distribution_gpu.py.
 """
 import os
 
@@ -17,15 +20,24 @@ from scipy.stats import ks_2samp
 
 from flipcomplexityempirical_amd import graphs as G
 
-FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "native_rng_c1.npz")
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 STATS = ("cut", "nb", "pop1", "wait", "mean_cut", "mean_nb")
 P_MIN = 1e-3  # per comparison; the samples are fixed (seeded), so the outcome is deterministic
+CASES = [("c1", 0), ("c1", 1), ("sec11", 0), ("sec11", 1)]
 
 
-def c1_setup():
-    spec = G.grid_graph(10, 10)
-    a0 = spec.assignment_array(G.threshold_plan(spec.nodes, 0, 5), [-1, 1])
-    _, (lo, hi) = G.population_bounds(100, 2, 0.1)
+def fixture(cfg):
+    return np.load(os.path.join(GOLD, f"native_rng_{cfg}.npz"))
+
+
+def setup(cfg):
+    if cfg == "c1":
+        spec = G.grid_graph(10, 10)
+        a0 = spec.assignment_array(G.threshold_plan(spec.nodes, 0, 5), [-1, 1])
+    else:
+        spec = G.sec11_graph()
+        a0 = spec.assignment_array(G.sec11_plan(2, spec.nodes), [-1, 1])
+    _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
     return spec, a0, lo, hi
 
 
@@ -48,17 +60,17 @@ def assert_same_distribution(fix, bi, got, label):
         assert p > P_MIN, (label, s, p, ref.mean(), got[s].mean())
 
 
-@pytest.mark.parametrize("bi", [0, 1])
-def test_canonical_oracle_matches_native_rng(cref, bi):
-    fix = np.load(FIX)
+@pytest.mark.parametrize("cfg,bi", CASES)
+def test_canonical_oracle_matches_native_rng(cref, cfg, bi):
+    fix = fixture(cfg)
     T, base = int(fix["T"]), float(fix["bases"][bi])
-    spec, a0, lo, hi = c1_setup()
+    spec, a0, lo, hi = setup(cfg)
     finals, waits, sc, sn = [], [], [], []
     for c in range(600):
         r = cref.run(spec, a0, base=base, pop_lo=lo, pop_hi=hi, seed=0xD15, chain_id=c, n_steps=T,
-                     log1mp=G.log1mp_table(100, 2))
+                     log1mp=G.log1mp_table(spec.n, 2))
         finals.append(r["final"])
         waits.append(r["stats"]["wait_cur"])
         sc.append(r["stats"]["sum_cut"])
         sn.append(r["stats"]["sum_nb"])
-    assert_same_distribution(fix, bi, summarize(spec, finals, waits, sc, sn, T), "C oracle")
+    assert_same_distribution(fix, bi, summarize(spec, finals, waits, sc, sn, T), f"C oracle {cfg}")
