@@ -7,6 +7,6 @@ for d in sorted(glob.glob(os.path.join(root, "b*_g*"))):
         continue
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if "flip_kernel" in r["Kernel_Name"]:
+        if "flip" in r["Kernel_Name"] and "kernel" in r["Kernel_Name"]:
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     print(os.path.basename(d), {k: f"{sum(v[1:]) / max(1, len(v) - 1):.4g}" for k, v in sorted(acc.items())})
