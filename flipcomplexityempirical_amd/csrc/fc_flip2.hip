@@ -234,6 +234,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
 
         while (pos < end) {
             FC_PROF(6, 1);
+            FC_STAMP(t_it0);
             // re-derive the predicates each iteration: loop-invariant lane values would otherwise
             // be hoisted as lane masks into SGPRs and spilled
             asm volatile("" : "+v"(st), "+v"(inA), "+v"(tmask), "+v"(nbr), "+v"(delta), "+v"(nA), "+v"(av), "+v"(pv),
@@ -298,6 +299,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 }
             }
             const uint64_t C0 = __ballot(valid && acc_now);
+            FC_STAMP(t_it1);
+            FC_PROF(8, t_it1 - t_it0);
             if (__popcll(C0) >= p.par_min) {
                 FC_PROF(12, 1);
                 // ---- segment-parallel commit ---------------------------------------------
@@ -430,6 +433,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     last_flip = rl32(v, L);
                     compiler_fence();
                 }
+                FC_STAMP(t_sg1);
+                FC_PROF(11, t_sg1 - t_it1);
                 pos = ce;
                 if (last_step) {
                     end = pos;
@@ -469,6 +474,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             }
             // ---- accept lane f: apply the flip -------------------------------------------------
             FC_PROF(7, 1);
+            FC_STAMP(t_ap0);
+            FC_PROF(9, t_ap0 - t_it1);
             const int vf = rl32(v, f), Af = rl32(av, f), pvf = rl32(pv, f), df = rl32(delta, f);
             const uint32_t inAf = rlu(inA, f), nbrf = rlu(nbr, f), tmf = rlu(tmask, f);
             const bool gamf = rl32((int)gam, f) != 0;
@@ -544,6 +551,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 nb_after = nb;
             }
             compiler_fence();
+            FC_STAMP(t_ap1);
+            FC_PROF(10, t_ap1 - t_ap0);
             pos = f + 1;
             if (rem == 0) {
                 end = pos;

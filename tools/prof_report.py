@@ -17,9 +17,12 @@ for g in range(G):
     b = max(x[5], 1)
     print(f"{g:3d}  {x[0]/1e6:9.2f}  {x[5]:8.0f} {x[7]:8.0f} {x[6]:9.0f} | {x[1]/b:8.0f} {x[2]/b:5.0f} {x[3]/b:7.0f} {x[4]/b:5.0f} | {x[3]/max(x[7],1):8.0f}")
 if S == 16:
-    print("grp | per iteration: verdict | one-event classify/apply per applied | parallel per segment, segments/batch")
+    print("grp | per iteration: verdict | one-event classify/apply per one-event flip | per segment, segments/batch | share: verdict one-event segment other")
     for g in range(G):
         x = last[np.arange(C) % G == g].mean(axis=0)
         it = max(x[6], 1)
-        print(f"{g:3d} | {x[8]/it:8.0f} | {x[9]/max(x[7],1):8.0f} {x[10]/max(x[7],1):8.0f} | {x[11]/max(x[12],1):8.0f} {x[12]/max(x[5],1):6.2f}")
+        ncm = max(x[3], 1)
+        oe = max(x[7] - 0, 1)
+        print(f"{g:3d} | {x[8]/it:8.0f} | {x[9]/oe:8.0f} {x[10]/oe:8.0f} | {x[11]/max(x[12],1):8.0f} {x[12]/max(x[5],1):6.2f}"
+              f" | {x[8]/ncm:5.2f} {(x[9]+x[10])/ncm:5.2f} {x[11]/ncm:5.2f} {1-(x[8]+x[9]+x[10]+x[11])/ncm:5.2f}")
 print("max chain total Mcyc", last[:, 0].max() / 1e6, "argmax", int(last[:, 0].argmax()))
