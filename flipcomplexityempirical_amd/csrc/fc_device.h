@@ -80,20 +80,23 @@ __device__ __forceinline__ bool one_run(uint32_t nbrA, uint32_t brk, uint32_t fu
     return cnt <= 1;
 }
 
-// BFS scratch of one chain (LDS): 4-bit source labels of the visited nodes, per-label
-// merge and component masks, the visited / frontier bitmaps, and a compaction buffer that
-// deals each level's frontier out to the lanes in chunks of kBfsChunk nodes.
-constexpr int kBfsChunk = 256;
+// BFS scratch of one chain (LDS): the source label of every visited node (one byte:
+// claimed nodes have exactly one writer, so plain stores), per-label merge and component
+// masks, the visited bitmap, two frontier lists (ping-pong; a level's claimers append to the
+// next one) and frontier bitmaps for the nodes that overflow a list.
+constexpr int kBfsList = 512;
 struct BfsScratch {
-    uint32_t *lab;    // [lab_words] nibbles: source label 0..15 of a visited node
+    uint32_t *lab;    // [lab_words] bytes: source label 0..15 of a visited node
     uint32_t *mm;     // [16] labels that label i ran into this level
     uint32_t *cm;     // [16] component mask of label i
-    uint16_t *list;   // [kBfsChunk] frontier chunk
+    int32_t *lcnt;    // [2] list lengths (may exceed kBfsList: the rest is in the bitmap)
+    uint16_t *list;   // [2][kBfsList] frontier lists
     uint64_t *vis;    // [W] visited
-    uint64_t *front;  // [W]
-    uint64_t *nxt;    // [W]
+    uint64_t *front;  // [W] overflowed frontier nodes of this level
+    uint64_t *nxt;    // [W] overflowed frontier nodes of the next level
     int lab_words;    // u32 words of lab
     int W;            // ceil(n / 64)
+    int64_t *prof;    // FC_PHASE_PROF builds: phase accumulators (slot 15: expansion cycles)
 };
 
 __device__ __forceinline__ uint32_t or_reduce(uint32_t x) {
@@ -108,13 +111,16 @@ __device__ __forceinline__ uint32_t or_reduce(uint32_t x) {
 // searches that meet are merged (16-bit component masks, one per label).  It answers yes
 // once one component holds every label, and no once some component has no frontier left
 // -- a whole connected piece of A - v without all of them -- which usually comes long
-// before a single-source search would have exhausted A.  Each level's frontier is
-// compacted (word popcounts + a wave prefix sum) and dealt out lane by lane.
+// before a single-source search would have exhausted A.  A level's frontier is a list the
+// previous level appended to (wave prefix sums), dealt out one node per lane; a node's
+// expansion is branch-free over its ring slots, so its ring reads, its claims and its
+// label reads each go out together.  Nodes beyond a list's capacity go to a bitmap that
+// the next level expands too.
 template <int RMAX>
-__device__ __forceinline__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, const BfsScratch &S, int lane,
-                                         int vf, int A, int my_target, int64_t &levels) {
+__device__ __forceinline__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, const BfsScratch &S,
+                                         int lane, int vf, int A, int my_target, int64_t &levels) {
     const int W = S.W;
-    for (int i = lane; i < S.lab_words; i += kWave) S.lab[i] = 0;
+    uint8_t *const lab = (uint8_t *)S.lab;
     for (int i = lane; i < W; i += kWave) {
         S.vis[i] = 0;
         S.front[i] = 0;
@@ -124,94 +130,128 @@ __device__ __forceinline__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, co
         S.mm[lane] = 0;
         S.cm[lane] = 1u << lane;
     }
-    wave_sync();
     const bool src = my_target >= 0;
     const uint64_t SM = __ballot(src);
     const int ns = __popcll(SM);  // <= 16 (degree <= 16)
+    wave_sync();
     if (ns <= 1) return true;
     if (src) {
         const uint32_t lab_me = (uint32_t)count_below(SM);  // labels 0..ns-1
-        atomicOr(&S.lab[my_target >> 3], lab_me << ((my_target & 7) * 4));
+        lab[my_target] = (uint8_t)lab_me;
         atomicOr((unsigned long long *)&S.vis[my_target >> 6], 1ull << (my_target & 63));
-        atomicOr((unsigned long long *)&S.front[my_target >> 6], 1ull << (my_target & 63));
+        S.list[lab_me] = (uint16_t)my_target;
     }
     if (lane == 0) atomicOr((unsigned long long *)&S.vis[vf >> 6], 1ull << (vf & 63));
     const uint32_t all = (uint32_t)((1ull << ns) - 1ull);  // labels 0..ns-1
     uint32_t comp = lane < 16 ? (1u << lane) : 0u;        // component mask of label `lane`
+    bool spill_in = false;                                 // frontier nodes wait in S.front
+    int fcur = ns;                                         // list length of this level
     wave_sync();
-    for (;;) {
+    for (int cur = 0;; cur ^= 1) {
         ++levels;
         uint32_t live = 0;  // labels that claimed a node at this level
-        bool merged = false;
-        // frontier size and each lane's first rank (lane owns words lane, lane + 64, ...)
-        int cnt = 0;
-        for (int i = lane; i < W; i += kWave) cnt += __popcll(S.front[i]);
-        const int incl = wave_scan_incl(cnt);
-        const int F = __builtin_amdgcn_readlane(incl, 63);
+        bool merged = false, spill_out = false;
+        uint16_t *const lcur = S.list + cur * kBfsList, *const lnxt = S.list + (cur ^ 1) * kBfsList;
+        int fnext = 0;  // appended to the next list so far (wave-uniform)
+        // expand u (active lanes): claim every A neighbour at once (vis bit: the first
+        // claimant wins), winners write their label, then losers read the labels they ran
+        // into; returns the ring slots this lane won
+        auto expand = [&](int u, bool active, int (&wn)[RMAX]) -> uint32_t {
+            const uint32_t la = lab[u];
+            const uint32_t cla = S.cm[la & 15u];
+            const NodeRec<RMAX> rr = G[u];
+            const uint32_t nbr = active ? (uint32_t)(rr.meta >> kMetaNbrShift) & 0xffffu : 0u;
+            uint32_t cand = 0, won = 0;
+#pragma unroll
+            for (int j = 0; j < RMAX; ++j) {
+                wn[j] = ring_entry<RMAX>(rr.ring, j);
+                cand |= (((nbr >> j) & 1u) & (uint32_t)(a[wn[j]] == A)) << j;
+            }
+            uint64_t old[RMAX];
+#pragma unroll
+            for (int j = 0; j < RMAX; ++j) {
+                const uint64_t bit = ((cand >> j) & 1u) ? 1ull << (wn[j] & 63) : 0ull;
+                old[j] = bit ? atomicOr((unsigned long long *)&S.vis[wn[j] >> 6], bit) : 0ull;
+            }
+#pragma unroll
+            for (int j = 0; j < RMAX; ++j) {
+                won |= (uint32_t)(((cand >> j) & 1u) && !((old[j] >> (wn[j] & 63)) & 1ull)) << j;
+                if ((won >> j) & 1u) lab[wn[j]] = (uint8_t)la;
+            }
+            live |= won ? 1u << la : 0u;
+            compiler_fence();  // every winner's label store precedes the losers' reads
+            uint32_t hit = 0;
+#pragma unroll
+            for (int j = 0; j < RMAX; ++j) {
+                const bool lose = ((cand & ~won) >> j & 1u) && wn[j] != vf;
+                const uint32_t lj = lose ? lab[wn[j]] & 15u : la;
+                hit |= ((cla >> lj) & 1u) ? 0u : 1u << lj;
+            }
+            if (hit) {  // another component
+                atomicOr(&S.mm[la], hit);
+                merged = true;
+            }
+            return won;
+        };
 #ifdef FC_PHASE_PROF
-        levels += F - 1;  // diagnostic build: count expanded nodes instead of levels
+        const int64_t t_x0 = (int64_t)__builtin_amdgcn_s_memtime();
+        levels += fcur - 1;  // diagnostic build: count expanded list nodes instead of levels
 #endif
-        for (int base = 0; base < F; base += kBfsChunk) {
-            int r = incl - cnt;
-            for (int i = lane; i < W && r < base + kBfsChunk; i += kWave) {
-                uint64_t bits = S.front[i];
-                const int pc = __popcll(bits);
-                if (r + pc <= base) {
-                    r += pc;
-                    continue;
+        const int Fl = min(fcur, kBfsList);
+        for (int q0 = 0; q0 < Fl; q0 += kWave) {  // one node per lane, wave-uniform trip count
+            const int q = q0 + lane;
+            const bool active = q < Fl;
+            int wn[RMAX];
+            const uint32_t won = expand(active ? (int)lcur[q] : vf, active, wn);
+            const int nw = __popc(won);
+            const int incl = wave_scan_incl(nw);
+            int pos = fnext + incl - nw;
+            fnext += __builtin_amdgcn_readlane(incl, kWave - 1);
+#pragma unroll
+            for (int j = 0; j < RMAX; ++j) {
+                if (!((won >> j) & 1u)) continue;
+                if (pos < kBfsList) {
+                    lnxt[pos] = (uint16_t)wn[j];
+                } else {
+                    atomicOr((unsigned long long *)&S.nxt[wn[j] >> 6], 1ull << (wn[j] & 63));
+                    spill_out = true;
                 }
+                ++pos;
+            }
+        }
+        if (spill_in) {  // the overflow of the previous level, from its bitmap (rare)
+            if (lane == 0) S.lcnt[0] = fnext;
+            wave_sync();
+            for (int i = lane; i < W; i += kWave) {
+                uint64_t bits = S.front[i];
                 while (bits) {
                     const int b = __builtin_ctzll(bits);
                     bits &= bits - 1;
-                    if (r >= base && r < base + kBfsChunk) S.list[r - base] = (uint16_t)(i * 64 + b);
-                    ++r;
-                }
-            }
-            wave_sync();
-            const int m = min(kBfsChunk, F - base);
-            for (int q = lane; q < m; q += kWave) {
-                const int u = S.list[q];
-                const uint32_t la = (S.lab[u >> 3] >> ((u & 7) * 4)) & 15u;
-                const uint32_t cla = S.cm[la];
-                const NodeRec<RMAX> rr = G[u];
-                const uint32_t nbr = (uint32_t)(rr.meta >> kMetaNbrShift) & 0xffffu;
-                // three LDS round trips per node: claim every neighbour at once (vis bit:
-                // the first claimant wins), winners write their label, then losers read the
-                // labels they ran into (one wave: LDS in program order)
-                int wn[RMAX];
-                uint32_t cand = 0, won = 0;
+                    int wn[RMAX];
+                    const uint32_t won = expand(i * 64 + b, true, wn);
+                    int pos = won ? atomicAdd(&S.lcnt[0], __popc(won)) : 0;
 #pragma unroll
-                for (int j = 0; j < RMAX; ++j) {
-                    wn[j] = ring_entry<RMAX>(rr.ring, j);
-                    cand |= (uint32_t)(((nbr >> j) & 1u) && a[wn[j]] == A) << j;
-                }
-#pragma unroll
-                for (int j = 0; j < RMAX; ++j) {
-                    if (!((cand >> j) & 1u)) continue;
-                    const uint64_t bit = 1ull << (wn[j] & 63);
-                    const uint64_t old = atomicOr((unsigned long long *)&S.vis[wn[j] >> 6], bit);
-                    won |= (uint32_t)!(old & bit) << j;
-                }
-#pragma unroll
-                for (int j = 0; j < RMAX; ++j) {
-                    if (!((won >> j) & 1u)) continue;
-                    atomicOr(&S.lab[wn[j] >> 3], la << ((wn[j] & 7) * 4));
-                    atomicOr((unsigned long long *)&S.nxt[wn[j] >> 6], 1ull << (wn[j] & 63));
-                }
-                live |= won ? 1u << la : 0u;
-                compiler_fence();  // every winner's label store precedes the losers' reads
-#pragma unroll
-                for (int j = 0; j < RMAX; ++j) {
-                    if (!((cand & ~won) >> j & 1u) || wn[j] == vf) continue;
-                    const uint32_t nib = (S.lab[wn[j] >> 3] >> ((wn[j] & 7) * 4)) & 15u;
-                    if (!((cla >> nib) & 1u)) {  // another component
-                        atomicOr(&S.mm[la], 1u << nib);
-                        merged = true;
+                    for (int j = 0; j < RMAX; ++j) {
+                        if (!((won >> j) & 1u)) continue;
+                        if (pos < kBfsList) {
+                            lnxt[pos] = (uint16_t)wn[j];
+                        } else {
+                            atomicOr((unsigned long long *)&S.nxt[wn[j] >> 6], 1ull << (wn[j] & 63));
+                            spill_out = true;
+                        }
+                        ++pos;
                     }
                 }
             }
             wave_sync();
+            fnext = S.lcnt[0];
         }
+        wave_sync();
+#ifdef FC_PHASE_PROF
+        if (lane == 0 && S.prof)
+            atomicAdd((unsigned long long *)&S.prof[15],
+                      (unsigned long long)((int64_t)__builtin_amdgcn_s_memtime() - t_x0));
+#endif
         if (__any(merged)) {
             // comp(i) |= labels i touched, symmetric, then transitive closure (<= 4 rounds)
             const uint32_t adj = comp | (lane < 16 ? S.mm[lane] : 0u);
@@ -243,10 +283,15 @@ __device__ __forceinline__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, co
         // a component without a live label is closed: a piece of A - v missing some label
         const bool dead = lane < ns && (comp & live) == 0u;
         if (__any(dead)) return false;
-        for (int i = lane; i < W; i += kWave) {
-            S.front[i] = S.nxt[i];
-            S.nxt[i] = 0;
+        const bool so = __any(spill_out);
+        if (spill_in || so) {
+            for (int i = lane; i < W; i += kWave) {
+                S.front[i] = S.nxt[i];
+                S.nxt[i] = 0;
+            }
         }
+        spill_in = so;
+        fcur = fnext;
         wave_sync();
     }
 }

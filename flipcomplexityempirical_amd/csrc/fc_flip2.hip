@@ -52,11 +52,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     bs.lab_words = p.lab_words;
     bs.mm = bs.lab + p.lab_words;
     bs.cm = bs.mm + 16;
-    bs.list = (uint16_t *)(bs.cm + 16);
-    bs.vis = (uint64_t *)(bs.list + kBfsChunk);
+    bs.lcnt = (int32_t *)(bs.cm + 16);
+    bs.list = (uint16_t *)(bs.lcnt + 4);
+    bs.vis = (uint64_t *)(bs.list + 2 * kBfsList);
     bs.front = bs.vis + p.words;
     bs.nxt = bs.front + p.words;
     bs.W = p.words;
+    bs.prof = nullptr;
     uint32_t *slot = (uint32_t *)(bs.nxt + p.words);  // [4][64]: node, word1, word2, draw offset
     uint8_t *smark = (uint8_t *)(slot + 4 * 64);   // [npad] lowest slot of a segment flip at the node
     uint8_t *nmark = smark + npad;                 // [npad] ... having the node as a neighbour

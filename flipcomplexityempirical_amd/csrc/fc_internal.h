@@ -13,9 +13,9 @@ namespace fc {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;   // one chain per wave, 4 chains per 256-thread workgroup
 constexpr int kBigChainLds = 16 * 1024;  // above this, one chain per 64-thread workgroup (occupancy)
-// LDS bytes of one chain's BFS scratch (dev::BfsScratch): labels, masks, chunk, 3 bitmaps
-inline int bfs_lab_words(int n) { return ((n + 7) / 8 + 1) & ~1; }
-inline int bfs_bytes(int n) { return 4 * bfs_lab_words(n) + 128 + 2 * 256 + 24 * ((n + 63) / 64); }
+// LDS bytes of one chain's BFS scratch (dev::BfsScratch): labels, masks, counters, 2 lists, 3 bitmaps
+inline int bfs_lab_words(int n) { return ((n + 3) / 4 + 1) & ~1; }
+inline int bfs_bytes(int n) { return 4 * bfs_lab_words(n) + 128 + 16 + 2 * 2 * 512 + 24 * ((n + 63) / 64); }
 inline int waves_per_block(int chain_lds_bytes) { return chain_lds_bytes > kBigChainLds ? 1 : kWavesPerBlock; }
 constexpr int kMaxK = 2;            // districts held in ChainScalars (k = 2 fast path)
 constexpr int kMaxKGeneral = 32;    // districts of the general (PAIR) kernel
@@ -82,7 +82,7 @@ struct KParams {
     int32_t n, n_edges, n_chains, k;
     int32_t chain_lds_bytes;    // LDS bytes per chain
     int32_t words;              // ceil(n / 64) bitmap words
-    int32_t lab_words;          // BFS label nibbles, u32 words (even)
+    int32_t lab_words;          // BFS label bytes, in u32 words (even)
     uint32_t lemire_thresh;     // 2^32 mod n
     uint32_t chain_id_offset;
     uint32_t seed_lo, seed_hi;

@@ -54,11 +54,13 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
     bs.lab_words = p.lab_words;
     bs.mm = bs.lab + p.lab_words;
     bs.cm = bs.mm + 16;
-    bs.list = (uint16_t *)(bs.cm + 16);
-    bs.vis = (uint64_t *)(bs.list + kBfsChunk);
+    bs.lcnt = (int32_t *)(bs.cm + 16);
+    bs.list = (uint16_t *)(bs.lcnt + 4);
+    bs.vis = (uint64_t *)(bs.list + 2 * kBfsList);
     bs.front = bs.vis + p.words;
     bs.nxt = bs.front + p.words;
     bs.W = p.words;
+    bs.prof = nullptr;
     uint32_t *slot = (uint32_t *)(bs.nxt + p.words);  // [5][64]: node, word1, word2, draw offset, word3
     int32_t *popk = (int32_t *)(slot + 5 * 64);    // [32] district populations (KM = 0)
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
@@ -100,6 +102,7 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
 #ifdef FC_PHASE_PROF
     int64_t *prof_acc = (int64_t *)(base + p.chain_lds_bytes - kProfSlots * 8);
     if (lane < kProfSlots) prof_acc[lane] = 0;
+    bs.prof = prof_acc;
 #endif
     wave_sync();
     FC_STAMP(t_loop0);
