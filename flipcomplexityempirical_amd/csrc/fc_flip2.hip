@@ -47,14 +47,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     int8_t *a = (int8_t *)base;                    // [npad] district of each node
     uint8_t *fcnt = base + npad;                   // [npad] foreign neighbours of each node
     uint64_t *T = (uint64_t *)(base + 2 * npad);   // [2 RMAX + 2] acceptance thresholds by delta-cut
-    BfsScratch bs;                                  // BFS labels, masks, chunk, bitmaps
-    bs.lab = (uint32_t *)(T + (2 * RMAX + 2));
-    bs.lab_words = p.lab_words;
-    bs.mm = bs.lab + p.lab_words;
-    bs.cm = bs.mm + 16;
-    bs.lcnt = (int32_t *)(bs.cm + 16);
-    bs.list = (uint16_t *)(bs.lcnt + 4);
-    bs.vis = (uint64_t *)(bs.list + 2 * kBfsList);
+    BfsScratch bs{};                                // wave_bfs_single: the three bitmaps only
+    bs.vis = (uint64_t *)(T + (2 * RMAX + 2));
     bs.front = bs.vis + p.words;
     bs.nxt = bs.front + p.words;
     bs.W = p.words;
