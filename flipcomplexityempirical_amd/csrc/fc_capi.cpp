@@ -53,6 +53,8 @@ struct fc_run {
     uint32_t *d_tape = nullptr;
     int64_t tape_draws = 0;
     int64_t *d_prof = nullptr;  // FC_PHASE_PROF builds
+    uint32_t *d_eta = nullptr;  // k = 2: per-launch pace of the slowest chain (issue priorities)
+    int64_t n_flip_launches = 0;
     int32_t *d_eu = nullptr, *d_ev = nullptr;  // recom: canonical edge list
     uint64_t *d_recom_thresh = nullptr;        // recom: [2E+1] acceptance thresholds
     int8_t *d_ser_a0 = nullptr;  // FC_DIAG_SERIES: assignment at the series window start
@@ -89,7 +91,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc, r->d_edge_since,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events, r->d_prof, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events, r->d_prof, r->d_eta, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -555,6 +557,29 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.con_valid = r->p.con_valid;
     k.con_accept = r->p.con_accept;
     if (r->variant) k.par_min = kWaveSlots + 1;  // variants commit one event at a time
+    // k = 2: chains with a short boundary need many draws per proposal and set the launch
+    // time; they get the SIMD's issue priority over the chains sharing it (s_setprio 1/2/3
+    // below |B| = n/2, n/5, n/10).  Scheduling only:
+    // every chain's trajectory is unchanged.  FC_PRIO_DIV="d0,d1,d2" sets the divisors, "0" off.
+    int pd[3] = {2, 5, 10};
+    if (const char *e = std::getenv("FC_PRIO_DIV")) {
+        int d0 = 0, d1 = 0, d2 = 0;
+        if (std::sscanf(e, "%d,%d,%d", &d0, &d1, &d2) == 3 && d0 > 0 && d1 > 0 && d2 > 0) {
+            pd[0] = d0, pd[1] = d1, pd[2] = d2;
+        } else {
+            pd[0] = 0;
+        }
+    }
+    for (int i = 0; i < 3; ++i) k.prio_nb[i] = pd[0] > 0 && r->p.k == 2 ? k.n / pd[i] : 0;
+    // once a chain has taken 1/16 of its steps, its projected finish against the previous
+    // launch's slowest chain sets the priority instead: the stragglers get the issue slots
+    k.prio_th[0] = 0.9f, k.prio_th[1] = 1.0f, k.prio_th[2] = 1.1f;
+    if (const char *e = std::getenv("FC_PRIO_TH")) {
+        float t0 = 0, t1 = 0, t2 = 0;
+        if (std::sscanf(e, "%f,%f,%f", &t0, &t1, &t2) == 3) k.prio_th[0] = t0, k.prio_th[1] = t1, k.prio_th[2] = t2;
+    }
+    k.eta = nullptr;
+    k.eta_parity = 0;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : r->stream;
     k.prof = nullptr;
 #ifdef FC_PHASE_PROF
@@ -610,9 +635,20 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     }
     // the kernel keeps per-launch step and per-lane counters in 32 bits: launch in chunks
     constexpr int64_t kChunk = int64_t(1) << 24;
+    if (r->p.k == 2 && k.prio_nb[0] > 0 && k.prio_th[0] >= 0.0f) {  // FC_PRIO_TH=-1,..: |B| rule only
+        if (!r->d_eta) {
+            if (int rc = dalloc(&r->d_eta, 2)) return rc;
+            HIP_TRY(hipMemsetAsync(r->d_eta, 0, 2 * sizeof(uint32_t), s));
+        }
+        k.eta = r->d_eta;
+    }
     for (int64_t done = 0; done < n_steps; done += kChunk) {
         k.n_steps = std::min(kChunk, n_steps - done);
         if (max_draws <= 0) k.max_draws = 65536 * k.n_steps;
+        if (k.eta) {
+            k.eta_parity = (int32_t)(r->n_flip_launches++ & 1);
+            HIP_TRY(hipMemsetAsync(r->d_eta + k.eta_parity, 0, sizeof(uint32_t), s));
+        }
         const int e = r->p.k == 2 ? fc::launch_flip2(k, r->g.ring_max, s, r->kname, sizeof r->kname)
                                     : fc::launch_flip_k2(k, r->g.ring_max, s, r->kname, sizeof r->kname);
         if (e != 0) return fail(FC_ERR_HIP, std::string("flip kernel launch: ") + hipGetErrorString((hipError_t)e));

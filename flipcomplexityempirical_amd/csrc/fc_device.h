@@ -15,7 +15,13 @@ __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory")
 __device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 #ifdef FC_PHASE_PROF
+#ifdef FC_PHASE_SYNC  // drain outstanding memory first: each phase is charged its own latency
+#define FC_STAMP(t)                                                    \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");        \
+    const int64_t t = (int64_t)__builtin_amdgcn_s_memtime()
+#else
 #define FC_STAMP(t) const int64_t t = (int64_t)__builtin_amdgcn_s_memtime()
+#endif
 // accumulators live in the chain's LDS tail (prof_acc), so profiling adds no registers
 #define FC_PROF(i, x) \
     do { if (lane == 0) atomicAdd((unsigned long long *)&prof_acc[i], (unsigned long long)(int64_t)(x)); } while (0)

@@ -100,7 +100,34 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     wave_sync();
     FC_STAMP(t_loop0);
 
+    // issue priority among the waves sharing a SIMD (scheduling only: trajectories are
+    // unchanged).  The launch lasts as long as its slowest chain, so the chains projected to
+    // finish last get the issue slots: a chain's projected finish (elapsed / steps taken so
+    // far x steps to take) against the previous launch's slowest chain, or, before it has
+    // taken 1/16 of its steps, its |B| (a short boundary needs many draws per proposal).
+    int prio = 0;
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+    const float eta = p.eta ? (float)p.eta[p.eta_parity ^ 1] * (float)p.n_steps * (1.0f / 1024.0f) : 0.0f;
     while (rem > 0) {
+        if (p.prio_nb[0] > 0) {
+            const int done = (int)p.n_steps - rem;
+            int lv;
+            if (eta > 0.0f && done * 16 >= (int)p.n_steps) {
+                const float pr = (float)(__builtin_amdgcn_s_memrealtime() - rt0) * (float)p.n_steps / ((float)done * eta);
+                lv = (pr > p.prio_th[0]) + (pr > p.prio_th[1]) + (pr > p.prio_th[2]);
+            } else {
+                lv = (nb < p.prio_nb[0]) + (nb < p.prio_nb[1]) + (nb < p.prio_nb[2]);
+            }
+            if (lv != prio) {
+                prio = lv;
+                switch (lv) {
+                    case 0: __builtin_amdgcn_s_setprio(0); break;
+                    case 1: __builtin_amdgcn_s_setprio(1); break;
+                    case 2: __builtin_amdgcn_s_setprio(2); break;
+                    default: __builtin_amdgcn_s_setprio(3); break;
+                }
+            }
+        }
         FC_STAMP(t_a);
         FC_PROF(5, 1);
         if (draw >= draw_cap) {
@@ -712,6 +739,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     }
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
+    if (p.eta && rem == 0 && lane == 0) {  // this launch's pace, for the next one's priorities
+        const uint64_t el = __builtin_amdgcn_s_memrealtime() - rt0;
+        atomicMax(&p.eta[p.eta_parity], (uint32_t)min(el * 1024ull / (uint64_t)max((int)p.n_steps, 1), 0xffffffffull));
+    }
 #ifdef FC_PHASE_PROF
     wave_sync();
     if (p.prof && lane == 0)

@@ -124,6 +124,10 @@ struct KParams {
     int32_t accept;             // FC_ACCEPT_*
     uint32_t con_valid;         // FC_CON_* of the Validator
     uint32_t con_accept;        // FC_CON_* of the accept callable
+    int32_t prio_nb[3];         // k = 2: issue priority 1/2/3 below these |B| (0: off)
+    uint32_t *eta;              // k = 2: [2] slowest chain's s_memrealtime ticks per 1024 steps, by launch parity
+    int32_t eta_parity;         // this launch writes eta[parity] and reads eta[parity ^ 1]
+    float prio_th[3];           // ... projected-finish / previous launch thresholds for priority 1/2/3
 };
 
 // Diagnostic build (-DFC_PHASE_PROF): s_memtime cycles per kernel phase, per chain.
