@@ -100,8 +100,9 @@ def load(build_if_missing: bool = True):
     global _lib
     if _lib is not None:
         return _lib
-    path = _build.LIB
-    if build_if_missing and (not os.path.exists(path) or _build._stale()):
+    # FC_LIB_PATH: load this prebuilt library as is (A/B timing of two builds on one box)
+    path = os.environ.get("FC_LIB_PATH") or _build.LIB
+    if build_if_missing and "FC_LIB_PATH" not in os.environ and (not os.path.exists(path) or _build._stale()):
         if os.path.exists(_build.HIPCC):
             _build.build()
     if not os.path.exists(path):
