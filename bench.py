@@ -156,8 +156,9 @@ def cpu_baseline(seconds: float, cores: int, wname: str = "c2"):
                       f"{seconds:.0f} s each from the start plans; {props} proposals"}
 
 
-def c_oracle_rate(seconds: float, wname: str = "c2"):
-    """Single-core rate of the plain-C oracle on the same workload (extra, informational)."""
+def c_oracle_rate(seconds: float, wname: str = "c2", g0: int = 0, stride: int = 1):
+    """Single-core rate of the plain-C oracle on the same workload (extra, informational):
+    chains g0, g0 + stride, ... of 20,000 steps each until ``seconds`` have passed."""
     from flipcomplexityempirical_amd import graphs as G
     from oracle.flipref import CRef
     w = Workload(wname)
@@ -165,13 +166,29 @@ def c_oracle_rate(seconds: float, wname: str = "c2"):
     cref = CRef()
     _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), w.k, w.pct)
     l1 = G.log1mp_table(spec.n, w.k)
-    props, t0, g = 0, time.perf_counter(), 0
+    props, t0, g = 0, time.perf_counter(), g0
     while time.perf_counter() - t0 < seconds:
         r = cref.run(spec, w.init_of(g), base=w.base_of(g), pop_lo=lo, pop_hi=hi, seed=w.seed, chain_id=g,
                      n_steps=20000, log1mp=l1, k=w.k, labels=w.labels, proposal=w.proposal)
         props += r["stats"]["proposals"]
-        g += 1
+        g += stride
     return props / (time.perf_counter() - t0)
+
+
+def _c_oracle_worker(args):
+    sys.path.insert(0, ROOT)
+    return c_oracle_rate(*args)
+
+
+def c_oracle_allcores(seconds: float, cores: int, wname: str = "c2"):
+    """The strong CPU baseline: the plain-C oracle, one process per core,
+    process i running chains i, i + cores, ... (every base of the sweep is covered)."""
+    from concurrent.futures import ProcessPoolExecutor
+    with ProcessPoolExecutor(max_workers=cores) as ex:
+        rates = list(ex.map(_c_oracle_worker, [(seconds, wname, i, cores) for i in range(cores)]))
+    return {"value": float(sum(rates)), "unit": "proposals/s", "cores": cores, "kind": "port",
+            "sample": f"plain-C oracle (oracle/flipref.c), {cores} processes, chains of 20,000 steps for "
+                      f"{seconds:.0f} s each"}
 
 
 def main():
@@ -291,6 +308,7 @@ def main():
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cores, args.workload)
             out["cpu_baseline_c_oracle_1core"] = c_oracle_rate(min(5.0, args.cpu_seconds), args.workload)
+            out["cpu_baseline_c_oracle_allcores"] = c_oracle_allcores(min(5.0, args.cpu_seconds), cores, args.workload)
         except Exception as ex:  # report, never fake
             out["cpu_baseline"] = {"value": None, "error": repr(ex)}
     print(json.dumps(out), flush=True)

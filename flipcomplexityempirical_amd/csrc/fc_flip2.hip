@@ -53,8 +53,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     bs.nxt = bs.front + p.words;
     bs.W = p.words;
     bs.prof = nullptr;
-    uint32_t *slot = (uint32_t *)(bs.nxt + p.words);  // [4][64]: node, word1, word2, draw offset
-    uint8_t *smark = (uint8_t *)(slot + 4 * 64);   // [npad] lowest slot of a segment flip at the node
+    uint32_t *slot = (uint32_t *)(bs.nxt + p.words);  // [5][64]: node, word1, word2, draw offset, ring link | len
+    uint8_t *smark = (uint8_t *)(slot + 5 * 64);   // [npad] lowest slot of a segment flip at the node
     uint8_t *nmark = smark + npad;                 // [npad] ... having the node as a neighbour
     uint8_t *const dum = nmark + npad + (lane & 15);  // [16] sink for masked-off stores
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
@@ -89,6 +89,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     const bool force_bfs = (p.flags & FC_FLAG_FORCE_BFS) != 0;
     const bool want_wait = (p.diag & FC_DIAG_WAIT) != 0;
     const bool trace_on = FULL && p.trace && c < p.trace_chains;
+    // per-edge and per-node tallies are applied lane-parallel after the commit and need the
+    // flips of a batch to touch disjoint edges and nodes: with them, a stale view still ends
+    // the batch instead of being re-evaluated
+    const bool reeval_ok = !(FULL && (p.diag & (FC_DIAG_EDGES | FC_DIAG_FLIPS)));
 
     // per-lane accumulators, reduced once per launch
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
@@ -202,7 +206,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             inA |= (uint32_t)(a[cell[i]] == av) << i;
         }
         inA &= full;
-        const int tgt = 1 - av;                 // -1 * assignment, grid_chain_sec11.py:145
+        slot[256 + lane] = link | (Ln << 16);  // for re-evaluations inside the commit
+        // target district: 1 - av (-1 * assignment, grid_chain_sec11.py:145)
         const uint32_t nbrA = inA & nbr;        // old-district neighbours
         uint32_t tmask = nbr & ~inA;            // target-district neighbours
         int nA = __popc(nbrA);
@@ -236,12 +241,53 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         const int last_flip0 = last_flip;
         const int a_last0 = FULL && last_flip0 >= 0 ? (int)a[last_flip0] : 0;
         int cut_after = 0, nb_after = 0;
-        const int dp_l = av == 0 ? -pv : pv;            // pops0 change of this lane's flip
-        const int dg_l = gam ? (av == 0 ? -1 : 1) : 0;  // ngamma0 change
+        // pops0 change of this lane's flip, ngamma0 change (derived from av / st: a
+        // re-evaluation changes them)
+        auto dp_of = [&]() { return av == 0 ? -pv : pv; };
+        auto dg_of = [&]() { return (st & LF_GAM) ? (av == 0 ? -1 : 1) : 0; };
+
+        // A committed flip that changes the view of later slots (its node, or a node of their
+        // ring) no longer ends the batch: the slots from `from` on are evaluated again against
+        // the current state (phase 2 once more, from registers and LDS) and the commit goes
+        // on.  A slot whose node left the boundary is then a non-proposal draw, as it is in
+        // the one-draw-at-a-time chain.  The commit marks of the segment passes so far are
+        // cleared first: every slot's view is current again.
+        auto reeval = [&](int from) {
+            if (st & LF_WROTE) {
+                smark[v] = 0xff;
+#pragma unroll
+                for (int i = 0; i < RMAX; ++i) *(((nbr >> i) & 1u) ? &nmark[cell[i]] : dum) = 0xff;
+            }
+            st &= ~LF_WROTE;
+            compiler_fence();
+            if (has && lane >= from) {
+                const uint32_t lkl = slot[256 + lane];
+                const uint32_t lnk = lkl & 0xffffu, L2 = lkl >> 16;
+                const uint32_t fl = (1u << L2) - 1u;
+                av = a[v];
+                uint32_t ia = 0;
+#pragma unroll
+                for (int i = 0; i < RMAX; ++i) ia |= (uint32_t)(a[cell[i]] == av) << i;
+                inA = ia & fl;
+                const uint32_t nbA = inA & nbr;
+                tmask = nbr & ~inA;
+                nA = __popc(nbA);
+                delta = nA - __popc(tmask);
+                const uint32_t rot = L2 ? (((inA >> 1) | (inA << (L2 - 1))) & fl) : 0u;
+                const uint32_t lk = inA & rot & lnk;
+                const bool sl = one_run(nbA, fl & ~lk, fl);
+                const uint32_t vlink = (L2 >= 2 && (inA & 1u) && ((inA >> (L2 - 1)) & 1u)) ? (1u << (L2 - 1)) : 0u;
+                const bool sc = one_run(nbA, fl & ~(lk | vlink), fl);
+                const bool ac = mant53(slot[64 + lane], slot[128 + lane]) < T[delta + RMAX];
+                st = (st & (LF_EXACT | LF_GAM | LF_HAS | LF_FRZ)) | (tmask != 0u ? LF_HIT : 0u) | (ac ? LF_ACC : 0u) |
+                     (sl ? LF_SLIN : 0u) | (sc ? LF_SCYC : 0u);
+            }
+            compiler_fence();
+        };
 
         // contiguity undecided by the ring rule at lane f: wave BFS on the current state
         auto run_bfs = [&](int f) -> bool {
-            const uint32_t nbrAf = rlu(nbrA, f);
+            const uint32_t nbrAf = rlu(inA & nbr, f);
             int my_target = -1, start = -1;
 #pragma unroll
             for (int k2 = 0; k2 < RMAX / 2; ++k2) {
@@ -338,6 +384,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 // itself exact).  Flips committed one at a time (below) leave no marks: they cut
                 // the batch at every lane they affect themselves.
                 const bool cand0 = valid && acc;
+                const int dp_l = dp_of(), dg_l = dg_of();
                 const int x0 = cand0 ? dp_l : 0;
                 const int P = wave_scan_incl(x0) - x0;
                 const int Gp = count_below(__ballot(cand0 && dg_l > 0)) - count_below(__ballot(cand0 && dg_l < 0));
@@ -361,6 +408,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 }
                 const uint64_t K = __ballot(cand1) & lane_range(pos, sg);
                 int x = kWave;  // first lane that must not be committed
+                bool stale_seg = false;
                 if (K) {
                     const bool inK = (K >> lane) & 1ull;
                     if (inK) st |= LF_WROTE;
@@ -387,16 +435,20 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         need = need && again;
                         if (!__any(need)) break;
                     }
-                    // alpha (later proposals), entering non-hits and beta (later candidates)
-                    bool conf = hit && ms < lane;
+                    // alpha (later slots), entering non-hits and beta (later candidates)
+                    bool conf = has && ms < lane;
 #pragma unroll
                     for (int i = 0; i < RMAX; ++i) {
                         const bool nb_i = (nbr >> i) & 1u;
-                        conf |= hit && (int)smark[cell[i]] < lane;
+                        conf |= has && (int)smark[cell[i]] < lane;
                         conf |= inK && nb_i && mn[i] < lane;
                     }
                     const uint64_t XX = __ballot(conf && lane > pos && lane < end);
-                    if (XX) x = __builtin_ctzll(XX);
+                    if (XX) {
+                        x = __builtin_ctzll(XX);
+                        stale_seg = true;
+                        FC_PROF(13, 1);
+                    }
                     // non-hit draws whose node a committed flip pulls into the boundary would
                     // now be proposals: the batch ends before the first of them
                     int t = trunc_off;
@@ -411,11 +463,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         trunc_off = t;
                         const int e2 = __popcll(__ballot(has && off_l < t));
                         if (e2 < x) x = e2;
+                        if (e2 < end) end = e2;  // the batch ends before the first entering draw
+                        FC_PROF(14, 1);
                     }
                 }
                 const int ce = min(sg, x);  // commit lanes [pos, ce)
                 if (x < sg) last_step = false;
-                if (x < end) end = x;
+                if (!reeval_ok && x < end) end = x;
                 if (prop && lane < ce) st |= valid1 ? (cand1 ? (ST_VS | ST_AC) : ST_VS) : (ok1 ? ST_IP : ST_IC);
                 rem -= __popcll(VAL & bits_below(ce));
                 const uint64_t AP = K & bits_below(ce);
@@ -436,7 +490,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         *(nb_i ? &fcnt[cell[i]] : dum) = (uint8_t)(oldc[i] + (int)up - (int)dn);
                         dnb += nb_i ? (int)(up & (uint32_t)(oldc[i] == 0)) - (int)(dn & (uint32_t)(oldc[i] == 1)) : 0;
                     }
-                    *(me ? (uint8_t *)&a[v] : dum) = (uint8_t)tgt;
+                    *(me ? (uint8_t *)&a[v] : dum) = (uint8_t)(1 - av);
                     *(me ? &fcnt[v] : dum) = (uint8_t)nA;
                     const int pkd = me ? ((delta + 32) | ((dnb + 32) << 16)) : 0;
                     const int S = wave_scan_incl(pkd);
@@ -465,6 +519,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     break;
                 }
                 if (pos >= end) break;
+                if (reeval_ok && stale_seg && AP) {  // a committed flip changed the view of a later slot
+                    reeval(pos);
+                    continue;
+                }
                 if (u == pos) {
                     const bool res = run_bfs(u);
                     if (lane == u) st |= ST_BD | (res ? ST_BR : 0u);
@@ -528,9 +586,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             uint32_t eqm = 0;
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) eqm |= (uint32_t)(cell[i] == vf) << i;
-            const bool stale = hit && (v == vf || eqm != 0u);
+            const bool stale = has && (v == vf || eqm != 0u);
             const uint64_t aff = __ballot(stale && lane > f && lane < end);
-            if (aff) end = __builtin_ctzll(aff);
+            if (aff) {
+                FC_PROF(13, 1);
+                if (!reeval_ok) end = __builtin_ctzll(aff);
+            }
             uint64_t ent = __ballot(enter);
             const int dnb = __popcll(ent) - __popcll(__ballot(leave));
             // non-hit draws after f whose node just entered the boundary would now propose
@@ -550,6 +611,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     trunc_off = t_na;
                     const int e2 = __popcll(__ballot(has && off_l < t_na));
                     if (e2 < end) end = e2;
+                    FC_PROF(14, 1);
                 }
             }
             if (Af == 0) {
@@ -582,6 +644,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 target_hit = true;
                 break;
             }
+            if (reeval_ok && aff && pos < end) reeval(pos);
         }
         if (st & LF_WROTE) {  // clear this lane's marks for the next batch
             smark[v] = 0xff;
@@ -593,6 +656,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         FC_STAMP(t_d);
         FC_PROF(3, t_d - t_c);
 
+        FC_PROF(15, (end == ns && !target_hit && trunc_off == gen) ? 1 : 0);  // every slot committed
         // ---- 4. lane-parallel bookkeeping of the committed draws [0, end) ------------------
         const bool done = lane < end;
         const bool is_acc = (st & ST_AC) != 0;
@@ -643,7 +707,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     ev.v = (uint16_t)v;
                     ev.cut = (uint16_t)cut_after;
                     ev.nb = (uint16_t)nb_after;
-                    ev.target = (uint8_t)tgt;
+                    ev.target = (uint8_t)(1 - av);
                     ev.reserved = 0;
                     p.events[(size_t)c * p.ev_cap + idx] = ev;
                 }
@@ -681,7 +745,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 if (is_acc) {
                     const int64_t t_last = t_acc + run_len - 1;
                     const int64_t old = (int64_t)atomicExch(lf + v, (unsigned long long)t_last);
-                    atomicAdd((unsigned long long *)(ps + v), (unsigned long long)(-(int64_t)p.labels[tgt] * (t_last - old)));
+                    atomicAdd((unsigned long long *)(ps + v), (unsigned long long)(-(int64_t)p.labels[1 - av] * (t_last - old)));
                     atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
                 }
             }
@@ -711,7 +775,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     const bool valid = (st & ST_VS) != 0;
                     rr.draw = (int64_t)d;
                     rr.v = v;
-                    rr.flags = (valid ? (1 | (is_acc ? 2 : 0)) : ((st & ST_IC) ? 4 : 8)) | (tgt << 8);
+                    rr.flags = (valid ? (1 | (is_acc ? 2 : 0)) : ((st & ST_IC) ? 4 : 8)) | ((1 - av) << 8);
                     rr.cut = mine ? c_j : cut0;
                     rr.nb = mine ? n_j : nb0;
                     rr.wait = valid ? (mine ? (int64_t)w_j : wait_cur) : 0;

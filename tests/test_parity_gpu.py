@@ -158,3 +158,41 @@ def test_sharded_equals_unsharded(gpu, sec11):
         for k in ("steps", "proposals", "draws", "accepted", "sum_cut", "sum_wait", "cut", "nb"):
             assert np.array_equal(ps[k], fs[k][off:off + cnt]), k
         assert np.array_equal(part.state(), fa[off:off + cnt])
+
+
+@pytest.mark.parametrize("nsub,hit_stop", [(1, 64), (2, 32), (4, 12), (4, 64)])
+@pytest.mark.parametrize("lean", [True, False])
+def test_sec11_batch_shapes(gpu, cref, sec11, monkeypatch, nsub, hit_stop, lean):
+    """Every compiled draw-round count of the k = 2 kernel (FC_NSUB), the round cut-off
+    (FC_HIT_STOP) and the in-place re-evaluation of stale slots are scheduling choices only:
+    the lean instance (waits only) and the full instance (trace + histograms) stay bit-exact
+    against the oracle under each of them."""
+    monkeypatch.setenv("FC_NSUB", str(nsub))
+    monkeypatch.setenv("FC_HIT_STOP", str(hit_stop))
+    inits, bases = _configs(sec11, G.sec11_plan, G.SEC11_BASES, 30)
+    # full: trace + histograms, without the per-edge / per-node tallies, so that stale slot
+    # views are re-evaluated in place (the ALL_DIAG tests above cover the batch-ending form)
+    diag = _lib.FC_DIAG_WAIT if lean else (_lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST)
+    fg = FlipGraph(sec11)
+    (_, _), (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 2, 0.1)
+    cfg = RunConfig(seed=11, pop_lo=lo, pop_hi=hi, diag_mask=diag, trace_chains=0 if lean else 30,
+                    trace_cap=0 if lean else 200000)
+    run = FlipRun(fg, inits, cfg, bases=bases)
+    run.steps(1500)
+    run.steps(1500)
+    name = run.kernel_name()
+    assert f"flip2_kernel<8, {nsub}, {'false' if lean else 'true'}>" in name, name
+    st = run.stats()
+    fin = run.state()
+    if not lean:
+        ch, nh = run.hist()
+    for c in range(30):
+        ref = cref.run(sec11, inits[c], base=bases[c], pop_lo=lo, pop_hi=hi, seed=11, chain_id=c, n_steps=3000,
+                       log1mp=G.log1mp_table(sec11.n, 2), trace_cap=500000, want_hist=not lean)
+        for k in STAT_KEYS:
+            assert int(st[k][c]) == int(ref["stats"][k]), (nsub, hit_stop, lean, c, k)
+        assert np.array_equal(fin[c], ref["final"]), (nsub, hit_stop, lean, c)
+        if not lean:
+            tr, rt = run.trace(c), ref["trace"]
+            assert len(tr) == len(rt) and all((tr[f] == rt[f]).all() for f in ("draw", "v", "flags", "cut", "nb", "wait"))
+            assert np.array_equal(ch[c], ref["cut_hist"]) and np.array_equal(nh[c], ref["nb_hist"])

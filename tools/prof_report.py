@@ -25,4 +25,10 @@ if S == 16:
         oe = max(x[7] - 0, 1)
         print(f"{g:3d} | {x[8]/it:8.0f} | {x[9]/oe:8.0f} {x[10]/oe:8.0f} | {x[11]/max(x[12],1):8.0f} {x[12]/max(x[5],1):6.2f}"
               f" | {x[8]/ncm:5.2f} {(x[9]+x[10])/ncm:5.2f} {x[11]/ncm:5.2f} {1-(x[8]+x[9]+x[10]+x[11])/ncm:5.2f}")
+if S == 16:
+    print("grp | per batch: stale-view cut  entering-non-hit cut  all slots committed")
+    for g in range(G):
+        x = last[np.arange(C) % G == g].mean(axis=0)
+        b = max(x[5], 1)
+        print(f"{g:3d} | {x[13]/b:6.3f} {x[14]/b:6.3f} {x[15]/b:6.3f}")
 print("max chain total Mcyc", last[:, 0].max() / 1e6, "argmax", int(last[:, 0].argmax()))
