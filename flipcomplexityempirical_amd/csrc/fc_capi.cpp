@@ -546,13 +546,14 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.ev_cap = r->ev_cap;
     k.hit_lo = r->p.hit_lo;
     k.hit_hi = r->p.hit_hi;
-    // k = 2: up to four rounds of 64 draws per batch, no further round once 12 draws of the
+    // k = 2: up to four rounds of 64 draws per batch, no further round once 32 draws of the
     // batch hit the boundary (short-boundary chains, which set the launch time, draw 256 per
-    // batch; the others stop after one or two rounds).  C2 sweep on one MI355X: 2 rounds /
-    // 32 hits 10.7 ms per launch, 4 / 12 10.3 ms (4 / 8: 10.55, 4 / 16: 10.5, 4 / 24: 10.8)
+    // batch).  C2 sweeps on one MI355X, ms per launch: before stale slots were re-evaluated
+    // in place, 2 rounds / 32 hits 10.7, 4 / 12 10.3 (4 / 8 10.55, 4 / 24 10.8); with the
+    // re-evaluation, 4 / 12 9.33, 4 / 20..64 8.9-9.0, 2 / 32 10.3, 8 / 32..64 9.45-9.55
     k.nsub = r->p.k == 2 ? 4 : 1;
     if (const char *e = std::getenv("FC_NSUB")) k.nsub = std::atoi(e);
-    k.hit_stop = 12;
+    k.hit_stop = 32;
     if (const char *e = std::getenv("FC_HIT_STOP")) k.hit_stop = std::atoi(e);
     k.par_min = 3;
     if (const char *e = std::getenv("FC_PAR_MIN")) k.par_min = std::atoi(e);

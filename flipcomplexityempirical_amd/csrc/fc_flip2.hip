@@ -16,10 +16,12 @@
 //      planar run rule, population bound, delta-cut, Metropolis threshold;
 //   3. commit in draw order.  One event at a time when few slots of the batch accept: the
 //      first acceptance is applied and every later slot whose view it changed (the flipped
-//      node in its ring or as its node) ends the batch, as does the first later non-hit
-//      draw whose node it pulled into the boundary.  When many accept, a segment-parallel
-//      commit (commit marks in LDS + prefix scans, below) applies them in one pass.  Either
-//      way the committed sequence is the one-draw-at-a-time chain, bit for bit;
+//      node in its ring or as its node) is evaluated again against the new state; the first
+//      later non-hit draw whose node it pulled into the boundary ends the batch.  When many
+//      accept, a segment-parallel commit (commit marks in LDS + prefix scans, below) applies
+//      them in one pass.  Either way the committed sequence is the one-draw-at-a-time chain,
+//      bit for bit (with per-edge / per-node tallies on, a stale view ends the batch
+//      instead: those tallies need the flips of a batch to be disjoint);
 //   4. the per-yield diagnostics are accumulated lane-parallel from per-slot status bits.
 #include <hip/hip_runtime.h>
 

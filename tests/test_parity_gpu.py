@@ -160,7 +160,7 @@ def test_sharded_equals_unsharded(gpu, sec11):
         assert np.array_equal(part.state(), fa[off:off + cnt])
 
 
-@pytest.mark.parametrize("nsub,hit_stop", [(1, 64), (2, 32), (4, 12), (4, 64)])
+@pytest.mark.parametrize("nsub,hit_stop", [(1, 64), (2, 32), (4, 12), (4, 32), (4, 64)])
 @pytest.mark.parametrize("lean", [True, False])
 def test_sec11_batch_shapes(gpu, cref, sec11, monkeypatch, nsub, hit_stop, lean):
     """Every compiled draw-round count of the k = 2 kernel (FC_NSUB), the round cut-off
