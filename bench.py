@@ -201,12 +201,15 @@ def main():
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--full-diag-steps", type=int, default=3,
+                    help="launches of the full-diagnostics side line (0: skip)")
     args = ap.parse_args()
 
     dist, rank, world, local_rank = _dist()
     import torch
     from flipcomplexityempirical_amd import graphs as G
     from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+    from flipcomplexityempirical_amd import _lib
 
     W = Workload(args.workload)
     spec = W.spec
@@ -303,6 +306,29 @@ def main():
                      "alg_bytes_per_launch": alg_bytes,
                      "lds": {"peak": LDS_PEAK_GBS, "frac": achieved / LDS_PEAK_GBS}},
     }
+    if world == 1 and args.full_diag_steps > 0:
+        # side line, outside the timed region above: the same workload with every per-yield
+        # tally of the driver loop on (grid_chain_sec11.py:366-402: cut / |B| histograms,
+        # per-edge cut_times, per-node num_flips / part_sum / last_flipped), FULL instance
+        run.close()
+        full = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
+        cfg_f = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
+                          chain_id_offset=int(off), device=local_rank, diag_mask=full)
+        rf = FlipRun(fg, inits, cfg_f, bases=bases)
+        rf.steps(args.chain_steps)
+        rf.sync()
+        f0 = rf.stats()
+        rf.timings()
+        t0f = time.perf_counter()
+        for _ in range(args.full_diag_steps):
+            rf.steps(args.chain_steps)
+        rf.sync()
+        dtf = time.perf_counter() - t0f
+        pf = float((rf.stats()["proposals"] - f0["proposals"]).sum())
+        out["full_diagnostics"] = {"value": pf / dtf, "unit": "proposals/s", "launches": args.full_diag_steps,
+                                   "kernel": rf.kernel_name(), "kernel_ms": float(rf.timings().mean()),
+                                   "diag": "waits + cut/|B| histograms + per-edge cut_times + per-node flips"}
+        rf.close()
     if world == 1 and not args.no_cpu_baseline:
         cores = min(16, os.cpu_count() or 1)
         try:
