@@ -43,7 +43,7 @@ struct fc_run {
     double *d_log1mp = nullptr;
     int32_t *d_labels = nullptr;
     int64_t *d_cut_hist = nullptr, *d_nb_hist = nullptr;
-    int64_t *d_edge_acc = nullptr, *d_edge_since = nullptr;
+    int64_t *d_edge_acc = nullptr;
     int64_t *d_num_flips = nullptr, *d_part_sum = nullptr, *d_last_flipped = nullptr;
     int32_t *d_popk = nullptr;
     int32_t wmax = 1;
@@ -90,7 +90,7 @@ int dalloc(T **p, size_t count) {
 void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
-                    r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc, r->d_edge_since,
+                    r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
                     r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events, r->d_prof, r->d_eta, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -432,9 +432,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     }
     if (want_edges) {
         if ((rc = dalloc(&r->d_edge_acc, (size_t)n_chains * E))) return rc;
-        if ((rc = dalloc(&r->d_edge_since, (size_t)n_chains * E))) return rc;
         HIP_TRY(hipMemset(r->d_edge_acc, 0, (size_t)n_chains * E * 8));
-        HIP_TRY(hipMemset(r->d_edge_since, 0, (size_t)n_chains * E * 8));
     }
     if (want_flips) {
         if ((rc = dalloc(&r->d_num_flips, (size_t)n_chains * n))) return rc;
@@ -533,7 +531,6 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.cut_hist = r->d_cut_hist;
     k.nb_hist = r->d_nb_hist;
     k.edge_acc = r->d_edge_acc;
-    k.edge_since = r->d_edge_since;
     k.num_flips = r->d_num_flips;
     k.part_sum = r->d_part_sum;
     k.last_flipped = r->d_last_flipped;
@@ -1032,11 +1029,10 @@ int fc_run_read_edges(fc_run *r, int64_t *cut_times) {
     if (!r->d_edge_acc) return fail(FC_ERR_ARG, "fc_run_read_edges: FC_DIAG_EDGES not enabled");
     if (int rc = fc_run_sync(r)) return rc;
     const size_t E = r->g.n_edges, C = r->n_chains;
-    std::vector<int64_t> acc(C * E), since(C * E);
+    std::vector<int64_t> acc(C * E);
     std::vector<int8_t> a(C * r->npad);
     std::vector<fc::ChainScalars> sc(C);
     HIP_TRY(hipMemcpy(acc.data(), r->d_edge_acc, acc.size() * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(since.data(), r->d_edge_since, since.size() * 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(a.data(), r->d_assign, a.size(), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
     for (size_t c = 0; c < C; ++c) {
@@ -1044,7 +1040,9 @@ int fc_run_read_edges(fc_run *r, int64_t *cut_times) {
         const int64_t T = sc[c].steps + 1;  // yields so far
         for (size_t e = 0; e < E; ++e) {
             const bool is_cut = ac[r->g.eu[e]] != ac[r->g.ev[e]];
-            cut_times[c * E + e] = acc[c * E + e] + (is_cut ? T - since[c * E + e] : 0);
+            // the kernels add the yield at which e turns uncut and subtract the one at which it
+            // turns cut; an edge cut now is cut through the last yield
+            cut_times[c * E + e] = acc[c * E + e] + (is_cut ? T : 0);
         }
     }
     return FC_OK;
@@ -1062,10 +1060,17 @@ int fc_run_read_flips(fc_run *r, int64_t *num_flips, int64_t *part_sum, int64_t 
     HIP_TRY(hipMemcpy(last_flipped, r->d_last_flipped, C * n * 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(a.data(), r->d_assign, a.size(), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    const int64_t lsum = (int64_t)r->labels[0] + (int64_t)r->labels[1];
     for (size_t c = 0; c < C; ++c) {
         const int64_t T = sc[c].steps + 1;
-        for (size_t u = 0; u < n; ++u)  // grid_chain_sec11.py:416-418
-            if (last_flipped[c * n + u] == 0) part_sum[c * n + u] = T * r->labels[a[c * r->npad + u]];
+        for (size_t u = 0; u < n; ++u) {
+            const int64_t lab = r->labels[a[c * r->npad + u]];
+            const int64_t t_r = last_flipped[c * n + u];
+            // k = 2 (fc_flip2.hip): every run of u added (L0 + L1 - 2 a_r) per yield; the last
+            // run's share is -a_R t_R instead
+            if (r->p.k == 2 && t_r != 0) part_sum[c * n + u] += (lab - lsum) * t_r;
+            if (t_r == 0) part_sum[c * n + u] = T * lab;  // grid_chain_sec11.py:416-418
+        }
     }
     return FC_OK;
 }

@@ -20,8 +20,7 @@
 //      later non-hit draw whose node it pulled into the boundary ends the batch.  When many
 //      accept, a segment-parallel commit (commit marks in LDS + prefix scans, below) applies
 //      them in one pass.  Either way the committed sequence is the one-draw-at-a-time chain,
-//      bit for bit (with per-edge / per-node tallies on, a stale view ends the batch
-//      instead: those tallies need the flips of a batch to be disjoint);
+//      bit for bit;
 //   4. the per-yield diagnostics are accumulated lane-parallel from per-slot status bits.
 #include <hip/hip_runtime.h>
 
@@ -91,10 +90,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     const bool force_bfs = (p.flags & FC_FLAG_FORCE_BFS) != 0;
     const bool want_wait = (p.diag & FC_DIAG_WAIT) != 0;
     const bool trace_on = FULL && p.trace && c < p.trace_chains;
-    // per-edge and per-node tallies are applied lane-parallel after the commit and need the
-    // flips of a batch to touch disjoint edges and nodes: with them, a stale view still ends
-    // the batch instead of being re-evaluated
-    const bool reeval_ok = !(FULL && (p.diag & (FC_DIAG_EDGES | FC_DIAG_FLIPS)));
 
     // per-lane accumulators, reduced once per launch
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
@@ -471,7 +466,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 }
                 const int ce = min(sg, x);  // commit lanes [pos, ce)
                 if (x < sg) last_step = false;
-                if (!reeval_ok && x < end) end = x;
                 if (prop && lane < ce) st |= valid1 ? (cand1 ? (ST_VS | ST_AC) : ST_VS) : (ok1 ? ST_IP : ST_IC);
                 rem -= __popcll(VAL & bits_below(ce));
                 const uint64_t AP = K & bits_below(ce);
@@ -521,7 +515,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     break;
                 }
                 if (pos >= end) break;
-                if (reeval_ok && stale_seg && AP) {  // a committed flip changed the view of a later slot
+                if (stale_seg && AP) {  // a committed flip changed the view of a later slot
                     reeval(pos);
                     continue;
                 }
@@ -590,10 +584,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             for (int i = 0; i < RMAX; ++i) eqm |= (uint32_t)(cell[i] == vf) << i;
             const bool stale = has && (v == vf || eqm != 0u);
             const uint64_t aff = __ballot(stale && lane > f && lane < end);
-            if (aff) {
-                FC_PROF(13, 1);
-                if (!reeval_ok) end = __builtin_ctzll(aff);
-            }
+            if (aff) FC_PROF(13, 1);
             uint64_t ent = __ballot(enter);
             const int dnb = __popcll(ent) - __popcll(__ballot(leave));
             // non-hit draws after f whose node just entered the boundary would now propose
@@ -646,7 +637,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 target_hit = true;
                 break;
             }
-            if (reeval_ok && aff && pos < end) reeval(pos);
+            if (aff && pos < end) reeval(pos);
         }
         if (st & LF_WROTE) {  // clear this lane's marks for the next batch
             smark[v] = 0xff;
@@ -734,34 +725,40 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             }
             if (p.diag & FC_DIAG_FLIPS) {
                 // part.flips is stale on rejected steps: every yield of a run repeats the update
-                // for the node whose flip created the state (grid_chain_sec11.py:396-400).
+                // part_sum[f] -= a[f] * (t - last_flipped[f]) for the node f whose flip created
+                // the state (grid_chain_sec11.py:396-400).  With two districts a node's label
+                // alternates between its runs, so summed over the runs r of f (last yield t_r,
+                // label a_r) part_sum = init - a_R t_R + sum_{r<R} (L0 + L1 - 2 a_r) t_r: every
+                // run adds (L0 + L1 - 2 a_r) per yield it lasts, and the read-out replaces the
+                // last run's share (fc_run_read_flips).  Only commuting adds and a max remain,
+                // so flips of one batch may share nodes.
                 int64_t *nf = p.num_flips + (size_t)c * n, *ps = p.part_sum + (size_t)c * n;
                 unsigned long long *lf = (unsigned long long *)(p.last_flipped + (size_t)c * n);
-                if (lane == 0 && r0 && last_flip0 >= 0) {
-                    const int64_t t_last = steps0 + r0;
-                    const int64_t old = (int64_t)atomicExch(lf + last_flip0, (unsigned long long)t_last);
-                    atomicAdd((unsigned long long *)(ps + last_flip0), (unsigned long long)(-(int64_t)p.labels[a_last0] * (t_last - old)));
+                const int64_t lsum = (int64_t)p.labels[0] + (int64_t)p.labels[1];
+                if (lane == 0 && r0 && last_flip0 >= 0) {  // the run of the batch's start state goes on
+                    atomicMax(lf + last_flip0, (unsigned long long)(steps0 + r0));
+                    atomicAdd((unsigned long long *)(ps + last_flip0), (unsigned long long)((lsum - 2 * (int64_t)p.labels[a_last0]) * r0));
                     atomicAdd((unsigned long long *)(nf + last_flip0), (unsigned long long)r0);
                 }
-                __builtin_amdgcn_s_waitcnt(0);
                 if (is_acc) {
                     const int64_t t_last = t_acc + run_len - 1;
-                    const int64_t old = (int64_t)atomicExch(lf + v, (unsigned long long)t_last);
-                    atomicAdd((unsigned long long *)(ps + v), (unsigned long long)(-(int64_t)p.labels[1 - av] * (t_last - old)));
+                    atomicMax(lf + v, (unsigned long long)t_last);
+                    atomicAdd((unsigned long long *)(ps + v), (unsigned long long)((lsum - 2 * (int64_t)p.labels[1 - av]) * t_last));
                     atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
                 }
             }
             if ((p.diag & FC_DIAG_EDGES) && is_acc) {
+                // cut_times[e] (yields with e cut, :383-384) = sum of the yields at which e turns
+                // uncut - sum of those at which it turns cut (+ the yield count while it is cut:
+                // fc_run_read_edges); commuting adds only
                 int64_t *ea = p.edge_acc + (size_t)c * p.n_edges;
-                unsigned long long *es = (unsigned long long *)(p.edge_since + (size_t)c * p.n_edges);
                 for (int i = 0; i < RMAX; ++i) {
                     if (!((nbr >> i) & 1u)) continue;
                     const int e = p.ring_eid[(size_t)v * RMAX + i];
                     if ((inA >> i) & 1u) {
-                        atomicExch(es + e, (unsigned long long)t_acc);             // becomes cut
+                        atomicAdd((unsigned long long *)(ea + e), (unsigned long long)(-t_acc));  // becomes cut
                     } else if ((tmask >> i) & 1u) {
-                        const int64_t since = (int64_t)atomicAdd(es + e, 0ull);    // becomes uncut
-                        atomicAdd((unsigned long long *)(ea + e), (unsigned long long)(t_acc - since));
+                        atomicAdd((unsigned long long *)(ea + e), (unsigned long long)t_acc);     // becomes uncut
                     }
                 }
             }

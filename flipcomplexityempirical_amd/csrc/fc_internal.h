@@ -101,7 +101,6 @@ struct KParams {
     int64_t *cut_hist;          // [n_chains * (E+1)]
     int64_t *nb_hist;           // [n_chains * (n+1)]
     int64_t *edge_acc;          // [n_chains * E]
-    int64_t *edge_since;        // [n_chains * E]
     int64_t *num_flips;         // [n_chains * n]
     int64_t *part_sum;          // [n_chains * n]
     int64_t *last_flipped;      // [n_chains * n]

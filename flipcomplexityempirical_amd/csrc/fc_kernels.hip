@@ -548,16 +548,16 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
                 }
             }
             if ((p.diag & FC_DIAG_EDGES) && is_acc) {
+                // cut_times[e] = sum of the yields at which e turns uncut - sum of those at which
+                // it turns cut (+ the yield count while it is cut: fc_run_read_edges)
                 int64_t *ea = p.edge_acc + (size_t)c * p.n_edges;
-                unsigned long long *es = (unsigned long long *)(p.edge_since + (size_t)c * p.n_edges);
                 for (int i = 0; i < RMAX; ++i) {
                     if (!((nbr >> i) & 1u)) continue;
                     const int e = p.ring_eid[(size_t)v * RMAX + i];
                     if ((inA >> i) & 1u) {
-                        atomicExch(es + e, (unsigned long long)t_acc);             // becomes cut
+                        atomicAdd((unsigned long long *)(ea + e), (unsigned long long)(-t_acc));  // becomes cut
                     } else if ((tmask >> i) & 1u) {
-                        const int64_t since = (int64_t)atomicAdd(es + e, 0ull);    // becomes uncut
-                        atomicAdd((unsigned long long *)(ea + e), (unsigned long long)(t_acc - since));
+                        atomicAdd((unsigned long long *)(ea + e), (unsigned long long)t_acc);     // becomes uncut
                     }
                 }
             }
