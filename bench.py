@@ -10,8 +10,9 @@ the exact sec11 graph of ``grid_chain_sec11.py:186-260`` (N = 1596, E = 3116), 4
 independent chains per GPU, chain c (global id g) with base ``bases[g % 10]``
 (``grid_chain_sec11.py:34``), start plan alignment ``(g // 10) % 3`` (``:195-214``),
 population tolerance 0.1 (``:319``), Philox seed 0x5EED0002.  One bench "step" is one
-launch advancing every chain by ``--chain-steps`` valid steps (default 10,000; 10 timed
-steps = the reference's 100,000-step run length).  Inputs are resident in HBM before the
+launch advancing every chain by ``--chain-steps`` valid steps (default 100,000 = one whole
+reference run, ``total_steps=100000`` at ``grid_chain_sec11.py:342``; 10 timed steps = the
+1e6 steps per chain of BASELINE config C2).  Inputs are resident in HBM before the
 timed region; the timed region is bracketed by barrier + device synchronisation.
 
 N > 1 (``torch.distributed.run``): one process per GPU, chains sharded by global id with
@@ -196,7 +197,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--chain-steps", type=int, default=10000)
+    ap.add_argument("--chain-steps", type=int, default=100000)
     ap.add_argument("--chains", type=int, default=0, help="chains per GPU (0: the workload's)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

@@ -14,7 +14,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 chains = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-chain_steps = int(sys.argv[3]) if len(sys.argv) > 3 else 10000
+chain_steps = int(sys.argv[3]) if len(sys.argv) > 3 else 100000
 src = os.path.join(ROOT, "gpurun_out")
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
