@@ -23,6 +23,9 @@
 //       lane-parallel from the per-lane status bits.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include <cstdio>
 
 #include "fc_internal.h"
@@ -648,7 +651,13 @@ __global__ __launch_bounds__(256) void flip_kernel(KParams p) {
 }
 
 int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap) {
-    const int wpb = waves_per_block(p.chain_lds_bytes);
+    // one chain (wave) per workgroup, as in fc_flip2.hip (C3 on one MI355X: 1.35e9 proposals/s
+    // against 1.29e9 with four chains per workgroup); FC_WPB = 2 / 4 restores larger ones
+    int wpb = 1;
+    if (const char *e = std::getenv("FC_WPB")) {
+        const int w = std::atoi(e);
+        if (w == 2 || w == 4) wpb = std::min(waves_per_block(p.chain_lds_bytes), w);
+    }
     const int blocks = (p.n_chains + wpb - 1) / wpb;
     const size_t lds = (size_t)p.chain_lds_bytes * wpb;
     hipStream_t s = (hipStream_t)stream;
