@@ -123,3 +123,21 @@ def test_c5_delaunay_k18_pair_parity(gpu, cref, n_points, steps):
     bases = np.asarray([0.5, 1.0, 2.0, 4.0] * 2)
     run = _run_pair(spec, inits, bases, k, steps=steps, pct=0.1)
     _check(cref, spec, run, k, inits, bases, steps=steps, pct=0.1)
+
+
+@pytest.mark.parametrize("graph", ["delaunay", "triangular"])
+def test_k2_irregular_graphs_parity(gpu, cref, graph):
+    """The k = 2 kernel off the square lattice: ring length 16 (Delaunay) or 6 (triangular),
+    nodes the planar rule leaves to the wave search, labels (0, 1), every per-yield tally on,
+    and stale slot views re-evaluated in place -- bit-exact against the oracle."""
+    if graph == "delaunay":
+        spec = G.delaunay_graph(1500, seed=0)
+        a0 = spec.assignment_array(G.bisection_plan(spec, 2), [0, 1])
+    else:
+        spec = G.triangular_graph(30, 58)
+        a0 = spec.assignment_array(G.strip_plan(spec, 2), [0, 1])
+    inits = np.stack([a0] * 8)
+    bases = np.asarray([0.5, 1.0, 2.0, 4.0] * 2)
+    run = _run_pair(spec, inits, bases, 2, steps=3000, pct=0.1, chunks=2, proposal=_lib.FC_PROPOSE_BI_SIGN)
+    assert "flip2_kernel" in run.kernel_name(), run.kernel_name()
+    _check(cref, spec, run, 2, inits, bases, steps=3000, pct=0.1)
