@@ -38,8 +38,11 @@ using namespace dev;
 
 // KM = 2: two districts (BI_SIGN, and PAIR with k = 2, which coincide); the outer-face
 // exact rule applies.  KM = 0: k <= 32 districts, PAIR proposals, populations in LDS.
+// RMAX = 8: at most 128 VGPRs, four waves per SIMD (C3's 8192 chains per GPU run in two
+// rounds of waves instead of three: 1.46e9 against 1.35e9 proposals/s; a handful of VGPRs
+// spill, which costs C4's LDS-limited launch 2 %)
 template <int RMAX, int NSUB, int KM, bool FULL>
-__global__ __launch_bounds__(256) void flip_kernel(KParams p) {
+__global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
