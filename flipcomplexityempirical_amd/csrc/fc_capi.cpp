@@ -283,8 +283,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: node degree above 16");
     if (recom)   // fc_recom.hip: best / spop, tree slots, component / levels, order, parent, a
         r->chain_lds_bytes = fc::recom_lds_bytes(n);
-    else if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, 3 BFS bitmaps, slots, commit marks (2 npad + 16)
-        r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16;
+    else if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, 3 BFS bitmaps, slots, commit marks (2 npad + 16),
+                      // wait queue (16 B per entry)
+        r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16 + fc::kWaitQ * 16;
     else         // fc_kernels.hip: a, fcnt, thresholds, BFS bitmaps, slots, district populations
         r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + fc::bfs_bytes(n) + 5 * 64 * 4 + fc::kMaxKGeneral * 4;
     r->wmax = 1;

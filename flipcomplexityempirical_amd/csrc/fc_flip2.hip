@@ -60,6 +60,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     uint8_t *smark = (uint8_t *)(slot + 5 * 64);   // [npad] lowest slot of a segment flip at the node
     uint8_t *nmark = smark + npad;                 // [npad] ... having the node as a neighbour
     uint8_t *const dum = nmark + npad + (lane & 15);  // [16] sink for masked-off stores
+    // lean instance: accepted states whose geometric wait is still to be drawn (kWaitQ of them:
+    // creating draw, |B| after the flip, yields so far); see wait_flush below
+    uint64_t *q_d = (uint64_t *)(nmark + npad + 16);
+    uint32_t *q_nb = (uint32_t *)(q_d + kWaitQ), *q_run = q_nb + kWaitQ;
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
     // ---- load the chain into LDS -------------------------------------------------------
@@ -83,6 +87,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     int pops0 = scp->pops[0], pops1 = scp->pops[1];
     int ng0 = scp->ngamma[0], ng1 = scp->ngamma[1];
     int64_t wait_cur = scp->wait_cur;
+    int qn = 0;  // queued accepted states (lean instance); the last one is the current state
     int last_flip = scp->last_flip;
     int stuck = 0;
     int rem = (int)p.n_steps;  // steps still to take in this launch (host: n_steps < 2^31)
@@ -108,6 +113,27 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     // finish last get the issue slots: a chain's projected finish (elapsed / steps taken so
     // far x steps to take) against the previous launch's slowest chain, or, before it has
     // taken 1/16 of its steps, its |B| (a short boundary needs many draws per proposal).
+    // The wait of an accepted state (geom_wait, grid_chain_sec11.py:147-148) only enters the
+    // run-length-weighted sum of waits, so the lean instance draws it later: a batch accepts
+    // 1-3 states, and a per-batch pass would run the purpose-1 Philox and the f64 log on a
+    // nearly idle wave in every chain's serial path.  The queue is drained by one full-width
+    // pass when it would overflow and at the end of the launch; the current state's wait is then
+    // known (wait_cur) and the yields it still lasts are charged to it directly.  The sums are
+    // the per-batch ones, term by term.
+    auto wait_flush = [&]() {
+        compiler_fence();
+        int64_t w = 0;
+        if (lane < qn) {
+            const uint64_t dq = q_d[lane];
+            const Words4 g = philox4x32_10((uint32_t)dq, (uint32_t)(dq >> 32), chain_gid, 1u, p.seed_lo, p.seed_hi);
+            w = geom_from(u53(g.x0, g.x1), p.log1mp[q_nb[lane]]);
+            acc_wait += w * (int64_t)q_run[lane];
+        }
+        wait_cur = (int64_t)(((uint64_t)(uint32_t)rl32((int)(uint32_t)w, qn - 1)) |
+                             ((uint64_t)(uint32_t)rl32((int)(w >> 32), qn - 1) << 32));
+        qn = 0;
+        compiler_fence();
+    };
     int prio = 0;
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
     const float eta = p.eta ? (float)p.eta[p.eta_parity ^ 1] * (float)p.n_steps * (1.0f / 1024.0f) : 0.0f;
@@ -668,7 +694,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         const int first_acc = ACCM ? __builtin_ctzll(ACCM) : end;
         const int r0 = __popcll(VSM & bits_below(first_acc));
         int64_t my_wait = 0;
-        if (want_wait && is_acc) {
+        if (FULL && want_wait && is_acc) {
             Words4 g;
             if (FULL && p.tape) {
                 const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + d) * 6;
@@ -683,14 +709,29 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             acc_cut2 += (int64_t)cut_after * cut_after * run_len;
             acc_nb += (int64_t)nb_after * run_len;
             acc_nb2 += (int64_t)nb_after * nb_after * run_len;
-            acc_wait += my_wait * run_len;
+            if (FULL) acc_wait += my_wait * run_len;
         }
         if (lane == 0 && r0) {
             acc_cut += (int64_t)cut0 * r0;
             acc_cut2 += (int64_t)cut0 * cut0 * r0;
             acc_nb += (int64_t)nb0 * r0;
             acc_nb2 += (int64_t)nb0 * nb0 * r0;
-            acc_wait += wait_cur * r0;
+            if (FULL || qn == 0) acc_wait += wait_cur * r0;  // else: the queued current state's run
+        }
+        if (!FULL && want_wait) {
+            if (lane == 0 && r0 && qn > 0) q_run[qn - 1] += (uint32_t)r0;
+            const int na = __popcll(ACCM);
+            if (na) {
+                if (qn + na > kWaitQ) wait_flush();
+                const int qi = qn + count_below(ACCM);
+                if (is_acc) {
+                    q_d[qi] = d;
+                    q_nb[qi] = (uint32_t)nb_after;
+                    q_run[qi] = (uint32_t)run_len;
+                }
+                qn += na;
+                compiler_fence();
+            }
         }
         if constexpr (FULL) {
             const int64_t t_acc = steps0 + __popcll(VSM & bits_below(lane + 1));  // yield index of this lane
@@ -784,7 +825,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 trace_len += __popcll(PM);
             }
         }
-        if (ACCM) {
+        if (FULL && ACCM) {
             const int la = 63 - __builtin_clzll(ACCM);
             wait_cur = (int64_t)(((uint64_t)(uint32_t)rl32((int)(uint32_t)my_wait, la)) |
                                  ((uint64_t)(uint32_t)rl32((int)(my_wait >> 32), la) << 32));
@@ -802,6 +843,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         FC_STAMP(t_e);
         FC_PROF(4, t_e - t_d);
     }
+    if (!FULL && qn > 0) wait_flush();
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
     if (p.eta && rem == 0 && lane == 0) {  // this launch's pace, for the next one's priorities

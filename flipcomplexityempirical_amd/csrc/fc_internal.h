@@ -134,6 +134,8 @@ struct KParams {
 //        6 commit-loop iterations, 7 applied flips; k = 2 commit detail: 8 verdicts,
 //        9 one-event classify, 10 one-event apply, 11 segment-parallel, 12 segments
 constexpr int kProfSlots = 16;
+// k = 2 lean kernel: accepted states queued for their geometric wait (fc_flip2.hip wait_flush)
+constexpr int kWaitQ = 64;
 
 // ReCom kernel parameters (fc_recom.hip).
 struct RecomParams {

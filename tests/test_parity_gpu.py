@@ -196,3 +196,25 @@ def test_sec11_batch_shapes(gpu, cref, sec11, monkeypatch, nsub, hit_stop, lean)
             tr, rt = run.trace(c), ref["trace"]
             assert len(tr) == len(rt) and all((tr[f] == rt[f]).all() for f in ("draw", "v", "flags", "cut", "nb", "wait"))
             assert np.array_equal(ch[c], ref["cut_hist"]) and np.array_equal(nh[c], ref["nb_hist"])
+
+
+@pytest.mark.parametrize("launches", [[5] * 12 + [37] * 8, [3000]])
+def test_sec11_lean_wait_queue(gpu, cref, sec11, launches):
+    """The lean k = 2 instance queues accepted states and draws their geometric waits later
+    (fc_flip2.hip wait_flush: on queue overflow and at the end of each launch).  Launches of a
+    few steps (the queue drained with the current state still running on) and one long launch
+    (many overflows) give the oracle's sum of waits and current wait bit for bit."""
+    inits, bases = _configs(sec11, G.sec11_plan, G.SEC11_BASES, 20)
+    fg = FlipGraph(sec11)
+    (_, _), (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 2, 0.1)
+    run = FlipRun(fg, inits, RunConfig(seed=13, pop_lo=lo, pop_hi=hi), bases=bases)
+    for n in launches:
+        run.steps(n)
+    assert "flip2_kernel<8, 4, false>" in run.kernel_name()
+    st = run.stats()
+    total = sum(launches)
+    for c in range(20):
+        ref = cref.run(sec11, inits[c], base=bases[c], pop_lo=lo, pop_hi=hi, seed=13, chain_id=c, n_steps=total,
+                       log1mp=G.log1mp_table(sec11.n, 2), trace_cap=0)
+        for k in ("steps", "accepted", "sum_wait", "wait_cur", "cut", "nb"):
+            assert int(st[k][c]) == int(ref["stats"][k]), (launches[0], c, k)

@@ -13,7 +13,10 @@ plans = [spec.assignment_array(G.sec11_plan(al, spec.nodes), [-1, 1]) for al in 
 inits = np.stack([plans[(c // 10) % 3] for c in range(C)])
 bases = np.asarray([G.SEC11_BASES[c % 10 if B < 0 else B] for c in range(C)])
 (_, _), (lo, hi) = G.population_bounds(1596, 2, 0.1)
-run = FlipRun(fg, inits, RunConfig(seed=0x5EED0002, pop_lo=lo, pop_hi=hi), bases=bases)
+# FC_PROBE_DIAG=<mask> overrides the diagnostics mask (0: no geometric waits)
+cfg = RunConfig(seed=0x5EED0002, pop_lo=lo, pop_hi=hi)
+if 'FC_PROBE_DIAG' in os.environ: cfg.diag_mask = int(os.environ['FC_PROBE_DIAG'])
+run = FlipRun(fg, inits, cfg, bases=bases)
 for it in range(IT):
     s0 = run.stats()
     t = time.time(); run.steps(S); run.sync(); dt = time.time() - t
