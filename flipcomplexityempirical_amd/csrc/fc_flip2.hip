@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     uint8_t *smark = (uint8_t *)(slot + 5 * 64);   // [npad] lowest slot of a segment flip at the node
     uint8_t *nmark = smark + npad;                 // [npad] ... having the node as a neighbour
     uint8_t *const dum = nmark + npad + (lane & 15);  // [16] sink for masked-off stores
-    // lean instance: accepted states whose geometric wait is still to be drawn (kWaitQ of them:
+    // accepted states whose geometric wait is still to be drawn (kWaitQ of them:
     // creating draw, |B| after the flip, yields so far); see wait_flush below
     uint64_t *q_d = (uint64_t *)(nmark + npad + 16);
     uint32_t *q_nb = (uint32_t *)(q_d + kWaitQ), *q_run = q_nb + kWaitQ;
@@ -97,6 +97,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     const bool force_bfs = (p.flags & FC_FLAG_FORCE_BFS) != 0;
     const bool want_wait = (p.diag & FC_DIAG_WAIT) != 0;
     const bool trace_on = FULL && p.trace && c < p.trace_chains;
+    // waits drawn later from the queue (wait_flush) unless a trace or a replay tape needs them per batch
+    const bool defer = want_wait && !trace_on && !(FULL && p.tape);
 
     // per-lane accumulators, reduced once per launch
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
@@ -114,7 +116,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     // far x steps to take) against the previous launch's slowest chain, or, before it has
     // taken 1/16 of its steps, its |B| (a short boundary needs many draws per proposal).
     // The wait of an accepted state (geom_wait, grid_chain_sec11.py:147-148) only enters the
-    // run-length-weighted sum of waits, so the lean instance draws it later: a batch accepts
+    // run-length-weighted sum of waits, so it is drawn later (no trace, no tape): a batch accepts
     // 1-3 states, and a per-batch pass would run the purpose-1 Philox and the f64 log on a
     // nearly idle wave in every chain's serial path.  The queue is drained by one full-width
     // pass when it would overflow and at the end of the launch; the current state's wait is then
@@ -694,7 +696,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         const int first_acc = ACCM ? __builtin_ctzll(ACCM) : end;
         const int r0 = __popcll(VSM & bits_below(first_acc));
         int64_t my_wait = 0;
-        if (FULL && want_wait && is_acc) {
+        if (FULL && want_wait && !defer && is_acc) {
             Words4 g;
             if (FULL && p.tape) {
                 const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + d) * 6;
@@ -709,16 +711,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             acc_cut2 += (int64_t)cut_after * cut_after * run_len;
             acc_nb += (int64_t)nb_after * run_len;
             acc_nb2 += (int64_t)nb_after * nb_after * run_len;
-            if (FULL) acc_wait += my_wait * run_len;
+            if (!defer) acc_wait += my_wait * run_len;
         }
         if (lane == 0 && r0) {
             acc_cut += (int64_t)cut0 * r0;
             acc_cut2 += (int64_t)cut0 * cut0 * r0;
             acc_nb += (int64_t)nb0 * r0;
             acc_nb2 += (int64_t)nb0 * nb0 * r0;
-            if (FULL || qn == 0) acc_wait += wait_cur * r0;  // else: the queued current state's run
+            if (!defer || qn == 0) acc_wait += wait_cur * r0;  // else: the queued current state's run
         }
-        if (!FULL && want_wait) {
+        if (defer) {
             if (lane == 0 && r0 && qn > 0) q_run[qn - 1] += (uint32_t)r0;
             const int na = __popcll(ACCM);
             if (na) {
@@ -825,7 +827,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 trace_len += __popcll(PM);
             }
         }
-        if (FULL && ACCM) {
+        if (!defer && ACCM) {
             const int la = 63 - __builtin_clzll(ACCM);
             wait_cur = (int64_t)(((uint64_t)(uint32_t)rl32((int)(uint32_t)my_wait, la)) |
                                  ((uint64_t)(uint32_t)rl32((int)(my_wait >> 32), la) << 32));
@@ -843,7 +845,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         FC_STAMP(t_e);
         FC_PROF(4, t_e - t_d);
     }
-    if (!FULL && qn > 0) wait_flush();
+    if (defer && qn > 0) wait_flush();
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
     if (p.eta && rem == 0 && lane == 0) {  // this launch's pace, for the next one's priorities

@@ -198,19 +198,22 @@ def test_sec11_batch_shapes(gpu, cref, sec11, monkeypatch, nsub, hit_stop, lean)
             assert np.array_equal(ch[c], ref["cut_hist"]) and np.array_equal(nh[c], ref["nb_hist"])
 
 
+@pytest.mark.parametrize("lean", [True, False])
 @pytest.mark.parametrize("launches", [[5] * 12 + [37] * 8, [3000]])
-def test_sec11_lean_wait_queue(gpu, cref, sec11, launches):
-    """The lean k = 2 instance queues accepted states and draws their geometric waits later
-    (fc_flip2.hip wait_flush: on queue overflow and at the end of each launch).  Launches of a
-    few steps (the queue drained with the current state still running on) and one long launch
-    (many overflows) give the oracle's sum of waits and current wait bit for bit."""
+def test_sec11_lean_wait_queue(gpu, cref, sec11, launches, lean):
+    """Without a trace or tape the k = 2 kernel (lean, or full with every tally but the trace)
+    queues accepted states and draws their geometric waits later (fc_flip2.hip wait_flush: on
+    queue overflow and at the end of each launch).  Launches of a few steps (the queue drained
+    with the current state still running on) and one long launch (many overflows) give the
+    oracle's sum of waits and current wait bit for bit."""
     inits, bases = _configs(sec11, G.sec11_plan, G.SEC11_BASES, 20)
     fg = FlipGraph(sec11)
     (_, _), (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 2, 0.1)
-    run = FlipRun(fg, inits, RunConfig(seed=13, pop_lo=lo, pop_hi=hi), bases=bases)
+    cfg = RunConfig(seed=13, pop_lo=lo, pop_hi=hi, diag_mask=_lib.FC_DIAG_WAIT if lean else ALL_DIAG)
+    run = FlipRun(fg, inits, cfg, bases=bases)
     for n in launches:
         run.steps(n)
-    assert "flip2_kernel<8, 4, false>" in run.kernel_name()
+    assert f"flip2_kernel<8, 4, {'false' if lean else 'true'}>" in run.kernel_name()
     st = run.stats()
     total = sum(launches)
     for c in range(20):
