@@ -286,8 +286,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     else if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, 3 BFS bitmaps, slots, commit marks (2 npad + 16),
                       // wait queue (16 B per entry)
         r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16 + fc::kWaitQ * 16;
-    else         // fc_kernels.hip: a, fcnt, thresholds, BFS bitmaps, slots, district populations
-        r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + fc::bfs_bytes(n) + 5 * 64 * 4 + fc::kMaxKGeneral * 4;
+    else         // fc_kernels.hip: a, fcnt, thresholds, BFS bitmaps, slots, district populations, wait queue
+        r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + fc::bfs_bytes(n) + 5 * 64 * 4 + fc::kMaxKGeneral * 4 +
+                             fc::kWaitQK * 16;
     r->wmax = 1;
     if (k > 2) r->wmax = p->wmax > 0 ? p->wmax : std::max(1, std::min(g.max_degree, k - 1));
 #ifdef FC_PHASE_PROF

@@ -136,6 +136,8 @@ struct KParams {
 constexpr int kProfSlots = 16;
 // k = 2 lean kernel: accepted states queued for their geometric wait (fc_flip2.hip wait_flush)
 constexpr int kWaitQ = 64;
+// k > 2 kernel: 32 entries, so that sec11 chains keep four waves per SIMD in 160 KB of LDS
+constexpr int kWaitQK = 32;
 
 // ReCom kernel parameters (fc_recom.hip).
 struct RecomParams {

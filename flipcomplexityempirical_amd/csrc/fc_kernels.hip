@@ -69,6 +69,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     bs.prof = nullptr;
     uint32_t *slot = (uint32_t *)(bs.nxt + p.words);  // [5][64]: node, word1, word2, draw offset, word3
     int32_t *popk = (int32_t *)(slot + 5 * 64);    // [32] district populations (KM = 0)
+    // accepted states whose geometric wait is still to be drawn (kWaitQK: creating draw, |B|
+    // after the flip, yields so far); as in fc_flip2.hip, drained by wait_flush
+    uint64_t *q_d = (uint64_t *)(popk + kMaxKGeneral);
+    uint32_t *q_nb = (uint32_t *)(q_d + kWaitQK), *q_run = q_nb + kWaitQK;
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
     // ---- load the chain into LDS -------------------------------------------------------
@@ -101,6 +105,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     const bool force_bfs = (p.flags & FC_FLAG_FORCE_BFS) != 0;
     const bool want_wait = (p.diag & FC_DIAG_WAIT) != 0;
     const bool trace_on = FULL && p.trace && c < p.trace_chains;
+    const bool defer = want_wait && !trace_on && !(FULL && p.tape);  // waits drawn later (wait_flush)
+    int qn = 0;
 
     // per-lane accumulators, reduced once per launch
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
@@ -110,6 +116,20 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     if (lane < kProfSlots) prof_acc[lane] = 0;
     bs.prof = prof_acc;
 #endif
+    // the k = 2 kernel's deferred waits (fc_flip2.hip): one full-width pass per queue load
+    auto wait_flush = [&]() {
+        compiler_fence();
+        int64_t w = 0;
+        if (lane < qn) {
+            const uint64_t dq = q_d[lane];
+            const Words4 g = philox4x32_10((uint32_t)dq, (uint32_t)(dq >> 32), chain_gid, 1u, p.seed_lo, p.seed_hi);
+            w = geom_from(u53(g.x0, g.x1), p.log1mp[q_nb[lane]]);
+            acc_wait += w * (int64_t)q_run[lane];
+        }
+        wait_cur = (int64_t)__shfl((long long)w, qn - 1);
+        qn = 0;
+        compiler_fence();
+    };
     wave_sync();
     FC_STAMP(t_loop0);
 
@@ -479,7 +499,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         const int first_acc = ACCM ? __builtin_ctzll(ACCM) : end;
         const int r0 = __popcll(VSM & bits_below(first_acc));
         int64_t my_wait = 0;
-        if (want_wait && is_acc) {
+        const int na = __popcll(ACCM);
+        // the start state's r0 further yields: its queue entry if it is queued, else wait_cur
+        const bool r0_queued = qn > 0;
+        if (lane == 0 && r0 && r0_queued) q_run[qn - 1] += (uint32_t)r0;
+        if (defer && na && qn + na > kWaitQK) wait_flush();
+        // a batch with more acceptances than the queue holds draws its waits now (queue empty)
+        const bool queue_now = defer && na <= kWaitQK;
+        if (want_wait && !queue_now && is_acc) {
             Words4 g;
             if (FULL && p.tape) {
                 const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + d) * 6;
@@ -495,14 +522,24 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             acc_cut2 += (int64_t)cut_after * cut_after * run_len;
             acc_nb += (int64_t)nb_after * run_len;
             acc_nb2 += (int64_t)nb_after * nb_after * run_len;
-            acc_wait += my_wait * run_len;
+            if (!queue_now) acc_wait += my_wait * run_len;
         }
         if (lane == 0 && r0) {
             acc_cut += (int64_t)cut0 * r0;
             acc_cut2 += (int64_t)cut0 * cut0 * r0;
             acc_nb += (int64_t)nb0 * r0;
             acc_nb2 += (int64_t)nb0 * nb0 * r0;
-            acc_wait += wait_cur * r0;
+            if (!r0_queued) acc_wait += wait_cur * r0;
+        }
+        if (queue_now && na) {
+            const int qi = qn + count_below(ACCM);
+            if (is_acc) {
+                q_d[qi] = d;
+                q_nb[qi] = (uint32_t)nb_after;
+                q_run[qi] = (uint32_t)run_len;
+            }
+            qn += na;
+            compiler_fence();
         }
         const int64_t t_acc = steps0 + __popcll(VSM & bits_below(lane + 1));  // yield index of this slot
         if (FULL && (p.diag & FC_DIAG_SERIES) && ACCM) {
@@ -587,12 +624,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             }
             trace_len += __popcll(P);
         }
-        if (ACCM) wait_cur = (int64_t)__shfl((long long)my_wait, 63 - __builtin_clzll(ACCM));
+        if (ACCM && !queue_now) wait_cur = (int64_t)__shfl((long long)my_wait, 63 - __builtin_clzll(ACCM));
         draw += (uint64_t)consumed;
         compiler_fence();
         FC_STAMP(t_e);
         FC_PROF(4, t_e - t_d);
     }
+    if (defer && qn > 0) wait_flush();
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
 #ifdef FC_PHASE_PROF

@@ -141,3 +141,29 @@ def test_k2_irregular_graphs_parity(gpu, cref, graph):
     run = _run_pair(spec, inits, bases, 2, steps=3000, pct=0.1, chunks=2, proposal=_lib.FC_PROPOSE_BI_SIGN)
     assert "flip2_kernel" in run.kernel_name(), run.kernel_name()
     _check(cref, spec, run, 2, inits, bases, steps=3000, pct=0.1)
+
+
+@pytest.mark.parametrize("launches", [[4] * 10 + [45] * 6, [2500]])
+def test_c3_lean_wait_queue(gpu, cref, sec11, launches):
+    """Without a trace or tape the general-k kernel queues accepted states (32 entries) and
+    draws their geometric waits later (fc_kernels.hip wait_flush); batches accepting more than
+    the queue holds draw them at once.  Short launches and one long launch give the oracle's
+    sum of waits and current wait bit for bit."""
+    k, n_chains = 4, 12
+    a0 = sec11.assignment_array(G.quadrant_plan(sec11.nodes), list(range(k)))
+    inits = np.stack([a0] * n_chains)
+    bases = np.asarray([[0.5, 1.0, G.SEC11_MU, 3.0][c % 4] for c in range(n_chains)])
+    fg = FlipGraph(sec11)
+    _, (lo, hi) = G.population_bounds(int(sec11.pop.sum()), k, 0.05)
+    cfg = RunConfig(k=k, labels=tuple(range(k)), proposal=_lib.FC_PROPOSE_PAIR, seed=23, pop_lo=lo, pop_hi=hi)
+    run = FlipRun(fg, inits, cfg, bases=bases)
+    for n in launches:
+        run.steps(n)
+    st = run.stats()
+    total = sum(launches)
+    for c in range(n_chains):
+        ref = cref.run(sec11, inits[c], base=float(bases[c]), pop_lo=lo, pop_hi=hi, seed=23, chain_id=c,
+                       n_steps=total, k=k, labels=list(range(k)), log1mp=G.log1mp_table(sec11.n, k),
+                       trace_cap=0, proposal=1)
+        for key in ("steps", "accepted", "sum_wait", "wait_cur", "cut", "nb"):
+            assert int(st[key][c]) == int(ref["stats"][key]), (launches[0], c, key)
