@@ -35,6 +35,8 @@ METRIC = "flip proposals/sec (node) 40x40 grid k=2, 1/2/4/8 MI355X; % LDS/HBM ro
 SEED = 0x5EED0002
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md chip-level parameters (spec)
 LDS_PEAK_GBS = 150000.0         # MI355X_MICROARCH.md §LDS: ~150 TB/s ds_read_b64/b128 aggregate
+# The chain state is LDS-resident (C1-C4 are LDS-bound; HBM only carries the
+# per-launch state load / store), so the roofline is priced against the LDS aggregate.
 # Algorithmic bytes: per proposal R = 2 + 1 + 8 + 5*deg + 5*L + 8 and per
 # accepted proposal W = 1 + 8 + 4*(deg+1) + 4 with deg = 4, L = 4 (sec11 interior).
 R_BYTES = 2 + 1 + 8 + 5 * 4 + 5 * 4 + 8      # 59
@@ -125,18 +127,24 @@ def _dist():
 
 
 def _cpu_worker(args):
-    """One chain of the same workload on the gerrychain-faithful Python port."""
-    gid, seconds, wname = args
+    """One chain of the same workload on a gerrychain-faithful Python port: ``native`` is
+    the reference's own proposal mechanism (``random.choice(list(b_nodes))``, :143, with
+    CPython / numpy Mersenne Twisters), ``philox`` the canonical-stream port."""
+    gid, seconds, wname, kind = args
     sys.path.insert(0, ROOT)
     from flipcomplexityempirical_amd import graphs as G
-    from oracle.flipref import GcFaithfulChain
+    from oracle.flipref import GcFaithfulChain, NativeRngChain
     w = Workload(wname)
     spec = w.spec
     a = w.init_of(gid)
     plan = {spec.nodes[i]: w.labels[int(a[i])] for i in range(spec.n)}
     (lo, hi), _ = G.population_bounds(int(spec.pop.sum()), w.k, w.pct)
-    ch = GcFaithfulChain(spec, plan, base=w.base_of(gid), pop_bounds=(lo, hi), seed=w.seed,
-                         chain_id=gid, log1mp=G.log1mp_table(spec.n, w.k), pair=w.k > 2)
+    if kind == "native":
+        ch = NativeRngChain(spec, plan, base=w.base_of(gid), pop_bounds=(lo, hi), seed=w.seed * 1000003 + gid,
+                            log1mp=G.log1mp_table(spec.n, w.k))
+    else:
+        ch = GcFaithfulChain(spec, plan, base=w.base_of(gid), pop_bounds=(lo, hi), seed=w.seed,
+                             chain_id=gid, log1mp=G.log1mp_table(spec.n, w.k), pair=w.k > 2)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         for _ in range(20):
@@ -145,16 +153,34 @@ def _cpu_worker(args):
     return ch.stats["proposals"], ch.stats["steps"], dt
 
 
-def cpu_baseline(seconds: float, cores: int, wname: str = "c2"):
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds: float, cores: int, wname: str = "c2", kind: str = "native"):
+    """The reference's Python CPU path on the host cores: one chain per process, chain ids
+    0..cores-1 of the workload (so every base of the C2 sweep is sampled), ``seconds`` each."""
     from concurrent.futures import ProcessPoolExecutor
     with ProcessPoolExecutor(max_workers=cores) as ex:
-        res = list(ex.map(_cpu_worker, [(g, seconds, wname) for g in range(cores)]))
+        res = list(ex.map(_cpu_worker, [(g, seconds, wname, kind) for g in range(cores)]))
     props = sum(r[0] for r in res)
     wall = max(r[2] for r in res)
+    what = ("the reference's flip step under its own random streams (oracle/flipref.py NativeRngChain: "
+            "random.choice(list(b_nodes)) at grid_chain_sec11.py:143, random() at :179, np.random.geometric "
+            "at :148, gerrychain-0.2 Partition / cut_edges / Dijkstra contiguity)" if kind == "native" else
+            "gerrychain-0.2-faithful Python restatement on the canonical Philox stream "
+            "(oracle/flipref.py GcFaithfulChain)")
     return {"value": props / wall, "unit": "proposals/s", "cores": cores, "kind": "port",
-            "sample": f"gerrychain-0.2-faithful Python restatement (oracle/flipref.py GcFaithfulChain), "
-                      f"{cores} processes x 1 chain of the same workload (chain ids 0..{cores - 1}) for "
-                      f"{seconds:.0f} s each from the start plans; {props} proposals"}
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": f"{what}; {cores} processes x 1 chain of the same workload (chain ids 0..{cores - 1}) "
+                      f"for {seconds:.0f} s each from the start plans; {props} proposals"}
 
 
 def c_oracle_rate(seconds: float, wname: str = "c2", g0: int = 0, stride: int = 1):
@@ -204,14 +230,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--full-diag-steps", type=int, default=3,
                     help="launches of the full-diagnostics side line (0: skip)")
+    ap.add_argument("--tune", default="",
+                    help="launch tuning, e.g. nsub=2,hit_stop=24,prio_div=2:5:10 (fc_params.tune_*; "
+                         "scheduling only)")
     args = ap.parse_args()
 
     dist, rank, world, local_rank = _dist()
     import torch
     from flipcomplexityempirical_amd import graphs as G
-    from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+    from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune
     from flipcomplexityempirical_amd import _lib
 
+    tune = parse_tune(args.tune) or None
     W = Workload(args.workload)
     spec = W.spec
     fg = FlipGraph(spec)
@@ -223,7 +253,7 @@ def main():
     bases = np.asarray([W.base_of(int(g)) for g in gids])
     _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), W.k, W.pct)
     cfg = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
-                    chain_id_offset=int(off), device=local_rank)
+                    chain_id_offset=int(off), device=local_rank, tune=tune)
     run = FlipRun(fg, inits, cfg, bases=bases)
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
@@ -248,6 +278,7 @@ def main():
     t1 = time.perf_counter()
     launch_ms = run.timings()
     s1 = run.stats()
+    kname = run.kernel_name()
 
     elapsed = t1 - t0
     props = float((s1["proposals"] - s0["proposals"]).sum())
@@ -265,6 +296,47 @@ def main():
     elapsed = D.allreduce_max(elapsed, dist, dev)
     kernel_ms = D.allreduce_max(kernel_ms, dist, dev)
     props, steps, acc = (float(agg[:, D.AGG_FIELDS.index(k)].sum()) for k in ("proposals", "steps", "accepted"))
+
+    full_out = None
+    if args.full_diag_steps > 0:
+        # side line, outside the timed region above and on every rank: the same workload with
+        # every per-yield tally of the reference's driver loop on (grid_chain_sec11.py:366-402:
+        # cut / |B| histograms, per-edge cut_times, per-node num_flips / part_sum /
+        # last_flipped), FULL instance; then the one §8(e) reduction of all of them
+        run.close()
+        full = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
+        cfg_f = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
+                          chain_id_offset=int(off), device=local_rank, diag_mask=full, tune=tune)
+        rf = FlipRun(fg, inits, cfg_f, bases=bases)
+        rf.steps(args.chain_steps)
+        barrier_sync_f = lambda: (rf.sync(), dist.barrier() if dist is not None else None)  # noqa: E731
+        barrier_sync_f()
+        f0 = rf.stats()
+        rf.timings()
+        t0f = time.perf_counter()
+        for _ in range(args.full_diag_steps):
+            rf.steps(args.chain_steps)
+        barrier_sync_f()
+        dtf = D.allreduce_max(time.perf_counter() - t0f, dist, dev)
+        kf = D.allreduce_max(float(rf.timings().mean()), dist, dev)
+        f1 = rf.stats()
+        ch, nh = rf.hist()
+        nf, ps, lf = rf.flips()
+        arrays = {"cut_hist": ch, "nb_hist": nh, "cut_times": rf.cut_times(), "num_flips": nf, "part_sum": ps,
+                  "last_flipped": lf}
+        red = D.allreduce_statistics(D.local_statistics(f1, gids % nb_, nb_, arrays), dist, dev)
+        pf = float((f1["proposals"] - f0["proposals"]).sum())
+        pf = float(D.allreduce_sum(np.asarray([pf]), dist, dev)[0])
+        yields = int(red["scalars"][:, D.AGG_FIELDS.index("steps")].sum()) + C * world
+        full_out = {"value": pf / dtf, "unit": "proposals/s", "launches": args.full_diag_steps,
+                    "kernel": rf.kernel_name(), "kernel_ms": kf,
+                    "diag": "waits + cut/|B| histograms + per-edge cut_times + per-node flips "
+                            "(the reference loop body's tallies, grid_chain_sec11.py:367-400)",
+                    "reduced": {"ranks": world, "collectives": "allreduce SUM (scalars, histograms, cut_times, "
+                                "num_flips, part_sum) + allreduce MAX (last_flipped)",
+                                "yields": yields, "cut_hist_mass": int(red["cut_hist"].sum()),
+                                "checksums": D.checksums(red)}}
+        rf.close()
 
     if rank != 0:
         if dist is not None:
@@ -294,46 +366,35 @@ def main():
         "data": "synthetic: the reference's sec11 lattice and start plans, Philox stream",
         "config": {"workload": W.desc, "graph": args.workload, "k": W.k, "chains_per_gpu": C,
                    "chain_steps_per_launch": args.chain_steps,
-                   "parallelism": f"chains sharded over {world} GPU(s)"},
+                   "parallelism": f"chains sharded over {world} GPU(s)", "tune": tune},
         "steps_per_s": steps / elapsed,
         "per_base_proposals_per_s": {f"{b:.4g}": float(agg[i, 0]) / elapsed for i, b in enumerate(W.bases)},
         "accept_per_proposal": acc / props if props else None,
         "draws_per_proposal": float(agg[:, D.AGG_FIELDS.index("draws")].sum()) / props if props else None,
         "bfs_per_proposal": float((s1["bfs_calls"] - s0["bfs_calls"]).sum()) * world / props if props else None,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": run.kernel_name(),
+        "roofline": {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / LDS_PEAK_GBS, "traffic": traffic,
+                     "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE "
+                                     "(profiles/pmc_traffic.json; gfx950 FETCH_SIZE doubled)",
+                     "kernel": kname,
                      "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": alg_bytes,
-                     "lds": {"peak": LDS_PEAK_GBS, "frac": achieved / LDS_PEAK_GBS}},
+                     "alg_bytes_per_proposal": W.R, "alg_bytes_per_accept": W.W,
+                     "hbm": {"peak": HBM_PEAK_GBS, "frac_alg": achieved / HBM_PEAK_GBS,
+                             "measured_gbs": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
+                             "frac_measured": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                             if traffic else None}},
     }
-    if world == 1 and args.full_diag_steps > 0:
-        # side line, outside the timed region above: the same workload with every per-yield
-        # tally of the driver loop on (grid_chain_sec11.py:366-402: cut / |B| histograms,
-        # per-edge cut_times, per-node num_flips / part_sum / last_flipped), FULL instance
-        run.close()
-        full = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
-        cfg_f = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
-                          chain_id_offset=int(off), device=local_rank, diag_mask=full)
-        rf = FlipRun(fg, inits, cfg_f, bases=bases)
-        rf.steps(args.chain_steps)
-        rf.sync()
-        f0 = rf.stats()
-        rf.timings()
-        t0f = time.perf_counter()
-        for _ in range(args.full_diag_steps):
-            rf.steps(args.chain_steps)
-        rf.sync()
-        dtf = time.perf_counter() - t0f
-        pf = float((rf.stats()["proposals"] - f0["proposals"]).sum())
-        out["full_diagnostics"] = {"value": pf / dtf, "unit": "proposals/s", "launches": args.full_diag_steps,
-                                   "kernel": rf.kernel_name(), "kernel_ms": float(rf.timings().mean()),
-                                   "diag": "waits + cut/|B| histograms + per-edge cut_times + per-node flips"}
-        rf.close()
+    if full_out is not None:
+        out["full_diagnostics"] = full_out
     if world == 1 and not args.no_cpu_baseline:
         cores = min(16, os.cpu_count() or 1)
         try:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cores, args.workload)
+            kind = "native" if W.k == 2 else "philox"
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cores, args.workload, kind)
+            if kind == "native":
+                out["cpu_baseline_philox_port"] = cpu_baseline(min(5.0, args.cpu_seconds), cores, args.workload,
+                                                               "philox")
             out["cpu_baseline_c_oracle_1core"] = c_oracle_rate(min(5.0, args.cpu_seconds), args.workload)
             out["cpu_baseline_c_oracle_allcores"] = c_oracle_allcores(min(5.0, args.cpu_seconds), cores, args.workload)
         except Exception as ex:  # report, never fake

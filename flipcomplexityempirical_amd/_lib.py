@@ -54,7 +54,12 @@ class Params(ctypes.Structure):
                 ("con_accept", ctypes.c_uint32), ("beta", ctypes.c_double), ("frozen", _P(ctypes.c_int32)),
                 ("n_frozen", ctypes.c_int32), ("recom_pop_target", ctypes.c_double),
                 ("recom_epsilon", ctypes.c_double), ("recom_node_repeats", ctypes.c_int32),
-                ("recom_max_attempts", ctypes.c_int32)]
+                ("recom_max_attempts", ctypes.c_int32),
+                # launch tuning (scheduling only; 0 = default)
+                ("tune_nsub", ctypes.c_int32), ("tune_hit_stop", ctypes.c_int32),
+                ("tune_par_min", ctypes.c_int32), ("tune_wait_queue", ctypes.c_int32),
+                ("tune_chains_per_block", ctypes.c_int32), ("tune_prio_div", ctypes.c_int32 * 3),
+                ("tune_prio_th", ctypes.c_float * 3)]
 
 
 class ChainStats(ctypes.Structure):

@@ -60,11 +60,18 @@ struct fc_run {
     int8_t *d_ser_a0 = nullptr;  // FC_DIAG_SERIES: assignment at the series window start
     char kname[96] = {0};        // last launched flip-kernel instance
     bool variant = false;        // accept / constraint variants (FULL k = 2 instance)
+    struct {                     // fc_params.tune_* with the defaults filled in
+        int32_t nsub, hit_stop, par_min, wait_q, wpb;
+        int32_t prio_div[3];     // prio_div[0] <= 0: priorities off
+        float prio_th[3];
+    } tune{};
+    size_t ev_head = 0;          // launch_events: oldest recorded pair (ring of kMaxLaunchEvents)
 };
 
 namespace {
 
 constexpr int kWaveSlots = 64;
+constexpr size_t kMaxLaunchEvents = 4096;  // per-launch HIP event pairs kept (fc_run_timings)
 thread_local std::string g_err;
 
 int fail(int code, const std::string &msg) {
@@ -297,6 +304,44 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     r->chain_lds_bytes = (r->chain_lds_bytes + 15) & ~15;
     if ((size_t)r->chain_lds_bytes * fc::waves_per_block(r->chain_lds_bytes) > 160 * 1024)
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: graph too large for the wave-per-chain LDS layout");
+
+    // ---- launch tuning (scheduling only; 0 = default) --------------------------------------
+    // k = 2: up to four rounds of 64 draws per batch, no further round once 32 draws of the
+    // batch hit the boundary (short-boundary chains, which set the launch time, draw 256 per
+    // batch).  C2 sweeps on one MI355X, ms per launch: before stale slots were re-evaluated
+    // in place, 2 rounds / 32 hits 10.7, 4 / 12 10.3 (4 / 8 10.55, 4 / 24 10.8); with the
+    // re-evaluation, 4 / 12 9.33, 4 / 20..64 8.9-9.0, 2 / 32 10.3, 8 / 32..64 9.45-9.55
+    {
+        auto &t = r->tune;
+        t.nsub = p->tune_nsub ? p->tune_nsub : (k == 2 ? 4 : 1);
+        if (!recom && !(k == 2 ? (t.nsub == 1 || t.nsub == 2 || t.nsub == 4) : (t.nsub == 1 || t.nsub == 2)))
+            return fail(FC_ERR_ARG, std::string("fc_run_create: tune_nsub must be ") +
+                                        (k == 2 ? "1, 2 or 4 for the k = 2 kernel" : "1 or 2 for the k > 2 kernel") +
+                                        " (got " + std::to_string(t.nsub) + ")");
+        t.hit_stop = p->tune_hit_stop ? p->tune_hit_stop : 32;
+        if (t.hit_stop < 1) return fail(FC_ERR_ARG, "fc_run_create: tune_hit_stop must be >= 1");
+        t.par_min = p->tune_par_min ? p->tune_par_min : 3;
+        if (t.par_min < 1) return fail(FC_ERR_ARG, "fc_run_create: tune_par_min must be >= 1");
+        const int qmax = k == 2 ? fc::kWaitQ : fc::kWaitQK;
+        t.wait_q = p->tune_wait_queue ? p->tune_wait_queue : qmax;
+        if (t.wait_q < 1 || t.wait_q > qmax)
+            return fail(FC_ERR_ARG, "fc_run_create: tune_wait_queue must be in [1, " + std::to_string(qmax) + "]");
+        t.wpb = p->tune_chains_per_block ? p->tune_chains_per_block : 1;
+        if (t.wpb != 1 && t.wpb != 2 && t.wpb != 4)
+            return fail(FC_ERR_ARG, "fc_run_create: tune_chains_per_block must be 1, 2 or 4");
+        t.wpb = std::min(t.wpb, fc::waves_per_block(r->chain_lds_bytes));
+        // k = 2: chains with a short boundary need many draws per proposal and set the launch
+        // time; they get the SIMD's issue priority over the chains sharing it (s_setprio 1/2/3
+        // below |B| = n/2, n/5, n/10); once a chain has taken 1/16 of its steps, its projected
+        // finish against the previous launch's slowest chain sets the priority instead
+        const bool div_default = !p->tune_prio_div[0] && !p->tune_prio_div[1] && !p->tune_prio_div[2];
+        for (int i = 0; i < 3; ++i) t.prio_div[i] = div_default ? (i == 0 ? 2 : i == 1 ? 5 : 10) : p->tune_prio_div[i];
+        if (t.prio_div[0] > 0 && (t.prio_div[1] <= 0 || t.prio_div[2] <= 0))
+            return fail(FC_ERR_ARG, "fc_run_create: tune_prio_div needs three positive divisors (or [0] < 0: off)");
+        const bool th_default = p->tune_prio_th[0] == 0.0f && p->tune_prio_th[1] == 0.0f && p->tune_prio_th[2] == 0.0f;
+        const float th0[3] = {0.9f, 1.0f, 1.1f};
+        for (int i = 0; i < 3; ++i) t.prio_th[i] = th_default ? th0[i] : p->tune_prio_th[i];
+    }
 
     // ---- host-side initial state (validated like MarkovChain.__init__ [gc-0.2]) ---------
     std::vector<int8_t> assign((size_t)n_chains * r->npad, 0);
@@ -545,42 +590,20 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.ev_cap = r->ev_cap;
     k.hit_lo = r->p.hit_lo;
     k.hit_hi = r->p.hit_hi;
-    // k = 2: up to four rounds of 64 draws per batch, no further round once 32 draws of the
-    // batch hit the boundary (short-boundary chains, which set the launch time, draw 256 per
-    // batch).  C2 sweeps on one MI355X, ms per launch: before stale slots were re-evaluated
-    // in place, 2 rounds / 32 hits 10.7, 4 / 12 10.3 (4 / 8 10.55, 4 / 24 10.8); with the
-    // re-evaluation, 4 / 12 9.33, 4 / 20..64 8.9-9.0, 2 / 32 10.3, 8 / 32..64 9.45-9.55
-    k.nsub = r->p.k == 2 ? 4 : 1;
-    if (const char *e = std::getenv("FC_NSUB")) k.nsub = std::atoi(e);
-    k.hit_stop = 32;
-    if (const char *e = std::getenv("FC_HIT_STOP")) k.hit_stop = std::atoi(e);
-    k.par_min = 3;
-    if (const char *e = std::getenv("FC_PAR_MIN")) k.par_min = std::atoi(e);
+    // launch tuning (fc_params.tune_*, resolved and checked by fc_run_create; scheduling only)
+    k.nsub = r->tune.nsub;
+    k.hit_stop = r->tune.hit_stop;
+    k.par_min = r->tune.par_min;
+    k.wait_q = r->tune.wait_q;
+    k.wpb = r->tune.wpb;
     k.variant = r->variant ? 1 : 0;
     k.accept = r->p.accept;
     k.con_valid = r->p.con_valid;
     k.con_accept = r->p.con_accept;
     if (r->variant) k.par_min = kWaveSlots + 1;  // variants commit one event at a time
-    // k = 2: chains with a short boundary need many draws per proposal and set the launch
-    // time; they get the SIMD's issue priority over the chains sharing it (s_setprio 1/2/3
-    // below |B| = n/2, n/5, n/10).  Scheduling only:
-    // every chain's trajectory is unchanged.  FC_PRIO_DIV="d0,d1,d2" sets the divisors, "0" off.
-    int pd[3] = {2, 5, 10};
-    if (const char *e = std::getenv("FC_PRIO_DIV")) {
-        int d0 = 0, d1 = 0, d2 = 0;
-        if (std::sscanf(e, "%d,%d,%d", &d0, &d1, &d2) == 3 && d0 > 0 && d1 > 0 && d2 > 0) {
-            pd[0] = d0, pd[1] = d1, pd[2] = d2;
-        } else {
-            pd[0] = 0;
-        }
-    }
-    for (int i = 0; i < 3; ++i) k.prio_nb[i] = pd[0] > 0 && r->p.k == 2 ? k.n / pd[i] : 0;
-    // once a chain has taken 1/16 of its steps, its projected finish against the previous
-    // launch's slowest chain sets the priority instead: the stragglers get the issue slots
-    k.prio_th[0] = 0.9f, k.prio_th[1] = 1.0f, k.prio_th[2] = 1.1f;
-    if (const char *e = std::getenv("FC_PRIO_TH")) {
-        float t0 = 0, t1 = 0, t2 = 0;
-        if (std::sscanf(e, "%f,%f,%f", &t0, &t1, &t2) == 3) k.prio_th[0] = t0, k.prio_th[1] = t1, k.prio_th[2] = t2;
+    for (int i = 0; i < 3; ++i) {
+        k.prio_nb[i] = r->tune.prio_div[0] > 0 && r->p.k == 2 ? k.n / r->tune.prio_div[i] : 0;
+        k.prio_th[i] = r->tune.prio_th[i];
     }
     k.eta = nullptr;
     k.eta_parity = 0;
@@ -593,13 +616,24 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     HIP_TRY(hipMemsetAsync(r->d_prof, 0, (size_t)r->n_chains * fc::kProfSlots * 8, s));
     k.prof = r->d_prof;
 #endif
-    if (r->n_launch_events == r->launch_events.size()) {
+    // per-launch event pairs: a pool that grows to kMaxLaunchEvents, then a ring that keeps
+    // the most recent ones (an iterator stepping one launch at a time never reads timings)
+    size_t slot_i;
+    if (r->n_launch_events < r->launch_events.size()) {
+        slot_i = (r->ev_head + r->n_launch_events) % r->launch_events.size();
+        ++r->n_launch_events;
+    } else if (r->launch_events.size() < kMaxLaunchEvents) {  // pool full and not wrapped (ev_head == 0)
         hipEvent_t a, b;
         HIP_TRY(hipEventCreate(&a));
         HIP_TRY(hipEventCreate(&b));
         r->launch_events.emplace_back(a, b);
+        slot_i = r->launch_events.size() - 1;
+        ++r->n_launch_events;
+    } else {  // ring full: overwrite the oldest
+        slot_i = r->ev_head;
+        r->ev_head = (r->ev_head + 1) % r->launch_events.size();
     }
-    auto &evp = r->launch_events[r->n_launch_events];
+    auto &evp = r->launch_events[slot_i];
     HIP_TRY(hipEventRecord(evp.first, s));
     if (r->p.proposal == FC_PROPOSE_RECOM) {
         fc::RecomParams q{};
@@ -633,13 +667,12 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
         HIP_TRY(hipEventRecord(evp.second, s));
         r->ev0 = evp.first;
         r->ev1 = evp.second;
-        ++r->n_launch_events;
         r->timed = true;
         return FC_OK;
     }
     // the kernel keeps per-launch step and per-lane counters in 32 bits: launch in chunks
     constexpr int64_t kChunk = int64_t(1) << 24;
-    if (r->p.k == 2 && k.prio_nb[0] > 0 && k.prio_th[0] >= 0.0f) {  // FC_PRIO_TH=-1,..: |B| rule only
+    if (r->p.k == 2 && k.prio_nb[0] > 0 && k.prio_th[0] >= 0.0f) {  // tune_prio_th[0] < 0: |B| rule only
         if (!r->d_eta) {
             if (int rc = dalloc(&r->d_eta, 2)) return rc;
             HIP_TRY(hipMemsetAsync(r->d_eta, 0, 2 * sizeof(uint32_t), s));
@@ -671,7 +704,6 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
 #endif
     r->ev0 = evp.first;
     r->ev1 = evp.second;
-    ++r->n_launch_events;
     r->timed = true;
     return FC_OK;
 }
@@ -694,15 +726,18 @@ int fc_run_last_ms(fc_run *r, float *ms) {
 int fc_run_timings(fc_run *r, float *ms, int32_t cap, int32_t *n) {
     if (!r || !n || (cap > 0 && !ms)) return fail(FC_ERR_ARG, "fc_run_timings: null argument");
     HIP_TRY(hipSetDevice(r->p.device));
-    const size_t cnt = r->n_launch_events;
-    if (cnt) HIP_TRY(hipEventSynchronize(r->launch_events[cnt - 1].second));
+    const size_t cnt = r->n_launch_events, sz = r->launch_events.size();
+    if (cnt) HIP_TRY(hipEventSynchronize(r->launch_events[(r->ev_head + cnt - 1) % sz].second));
     int32_t m = 0;
-    for (size_t i = 0; i < cnt && m < cap; ++i, ++m)
-        HIP_TRY(hipEventElapsedTime(&ms[m], r->launch_events[i].first, r->launch_events[i].second));
+    for (size_t i = 0; i < cnt && m < cap; ++i, ++m) {
+        const auto &pr = r->launch_events[(r->ev_head + i) % sz];
+        HIP_TRY(hipEventElapsedTime(&ms[m], pr.first, pr.second));
+    }
     *n = (int32_t)cnt;
-    // keep the most recent pair at slot 0 so fc_run_last_ms stays valid
-    if (cnt > 1) std::swap(r->launch_events[0], r->launch_events[cnt - 1]);
+    // the next launch records into slot 0 again; fc_run_last_ms keeps reading ev0 / ev1 (the
+    // most recent pair) until then
     r->n_launch_events = 0;
+    r->ev_head = 0;
     return FC_OK;
 }
 

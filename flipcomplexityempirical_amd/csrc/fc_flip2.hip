@@ -724,7 +724,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             if (lane == 0 && r0 && qn > 0) q_run[qn - 1] += (uint32_t)r0;
             const int na = __popcll(ACCM);
             if (na) {
-                if (qn + na > kWaitQ) wait_flush();
+                if (qn > 0 && qn + na > p.wait_q) wait_flush();  // na <= 64 = kWaitQ always fits an empty queue
                 const int qi = qn + count_below(ACCM);
                 if (is_acc) {
                     q_d[qi] = d;
@@ -916,12 +916,8 @@ int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_
     // bases differ, round-robin over the XCDs, CUs and SIMDs, and the short-boundary chains
     // that set the launch time spread more evenly over the SIMDs than four to a workgroup
     // (C2 on one MI355X: 8.46 ms per 10,000-step launch against 9.0 with four, 9.5 with two).
-    // FC_WPB = 2 / 4 restores the larger workgroups (diagnostic).
-    int wpb = 1;
-    if (const char *e = std::getenv("FC_WPB")) {
-        const int w = std::atoi(e);
-        if (w == 2 || w == 4) wpb = std::min(waves_per_block(p.chain_lds_bytes), w);
-    }
+    // tune_chains_per_block = 2 / 4 restores the larger workgroups (diagnostic).
+    const int wpb = p.wpb;  // fc_params.tune_chains_per_block (resolved by fc_run_create)
     const int blocks = (p.n_chains + wpb - 1) / wpb;
     const size_t lds = (size_t)p.chain_lds_bytes * wpb;
     hipStream_t s = (hipStream_t)stream;

@@ -127,6 +127,8 @@ struct KParams {
     uint32_t *eta;              // k = 2: [2] slowest chain's s_memrealtime ticks per 1024 steps, by launch parity
     int32_t eta_parity;         // this launch writes eta[parity] and reads eta[parity ^ 1]
     float prio_th[3];           // ... projected-finish / previous launch thresholds for priority 1/2/3
+    int32_t wait_q;             // deferred-wait queue capacity in use (<= kWaitQ / kWaitQK)
+    int32_t wpb;                // chains (waves) per workgroup: 1, 2 or 4
 };
 
 // Diagnostic build (-DFC_PHASE_PROF): s_memtime cycles per kernel phase, per chain.

@@ -501,11 +501,15 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         int64_t my_wait = 0;
         const int na = __popcll(ACCM);
         // the start state's r0 further yields: its queue entry if it is queued, else wait_cur
+        // (charged below, before anything can change wait_cur)
         const bool r0_queued = qn > 0;
         if (lane == 0 && r0 && r0_queued) q_run[qn - 1] += (uint32_t)r0;
-        if (defer && na && qn + na > kWaitQK) wait_flush();
+        if (lane == 0 && r0 && !r0_queued) acc_wait += wait_cur * r0;
+        // drain a non-empty queue that cannot take this batch (an empty one has nothing to
+        // draw, and its flush would leave wait_cur undefined)
+        if (defer && na && qn > 0 && qn + na > p.wait_q) wait_flush();
         // a batch with more acceptances than the queue holds draws its waits now (queue empty)
-        const bool queue_now = defer && na <= kWaitQK;
+        const bool queue_now = defer && na <= p.wait_q;
         if (want_wait && !queue_now && is_acc) {
             Words4 g;
             if (FULL && p.tape) {
@@ -529,7 +533,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             acc_cut2 += (int64_t)cut0 * cut0 * r0;
             acc_nb += (int64_t)nb0 * r0;
             acc_nb2 += (int64_t)nb0 * nb0 * r0;
-            if (!r0_queued) acc_wait += wait_cur * r0;
         }
         if (queue_now && na) {
             const int qi = qn + count_below(ACCM);
@@ -693,12 +696,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
 
 int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap) {
     // one chain (wave) per workgroup, as in fc_flip2.hip (C3 on one MI355X: 1.35e9 proposals/s
-    // against 1.29e9 with four chains per workgroup); FC_WPB = 2 / 4 restores larger ones
-    int wpb = 1;
-    if (const char *e = std::getenv("FC_WPB")) {
-        const int w = std::atoi(e);
-        if (w == 2 || w == 4) wpb = std::min(waves_per_block(p.chain_lds_bytes), w);
-    }
+    // against 1.29e9 with four chains per workgroup); tune_chains_per_block = 2 / 4 restores larger ones
+    const int wpb = p.wpb;  // fc_params.tune_chains_per_block (resolved by fc_run_create)
     const int blocks = (p.n_chains + wpb - 1) / wpb;
     const size_t lds = (size_t)p.chain_lds_bytes * wpb;
     hipStream_t s = (hipStream_t)stream;

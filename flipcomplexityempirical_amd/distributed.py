@@ -3,11 +3,22 @@
 Chains are independent: global chain id g = offset(rank) + c, and the Philox counter holds
 g, so every chain's trajectory is independent of how many GPUs run it.  There is no
 data-path collective; at the end one all-reduce (RCCL over xGMI with backend "nccl", gloo on
-CPU) sums the per-group statistics.
+CPU) sums every statistic the reference's driver accumulates (grid_chain_sec11.py:350-419):
+
+* per-group scalars (AGG_FIELDS: proposals, steps, accepted, invalid counts, the per-yield
+  sums behind rce / rbn / wait.txt);
+* the |cut| and |B| histograms over yields (E + 1 and N + 1 bins);
+* per-edge ``cut_times`` (:383-384, E entries);
+* per-node ``num_flips`` and ``part_sum`` (:396-400, N entries each);
+* per-node ``last_flipped`` (:398), reduced by MAX (the one non-additive field; it rides in
+  the same packed buffer as a second all-reduce with op MAX).
+
+The sum fields travel as one packed int64 buffer (<= ~100 KB for sec11), so the collective is
+latency-bound whatever the link: xGMI bandwidth is irrelevant here.
 """
 from __future__ import annotations
 
-from typing import Dict, Sequence, Tuple
+from typing import Dict, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -54,3 +65,78 @@ def allreduce_max(x: float, dist=None, device=None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# per-run arrays of the full diagnostics (FlipRun.hist / cut_times / flips), reduced over
+# chains on each rank and then over ranks
+SUM_ARRAYS = ("cut_hist", "nb_hist", "cut_times", "num_flips", "part_sum")
+MAX_ARRAYS = ("last_flipped",)
+
+
+def local_statistics(stats: Dict[str, np.ndarray], groups: np.ndarray, n_groups: int,
+                     arrays: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
+    """One rank's contribution: grouped scalar sums plus, for every per-chain array present
+    in ``arrays`` (``[chains, len]``), its sum (or max) over the rank's chains."""
+    out = {"scalars": group_aggregate(stats, groups, n_groups)}
+    for name, arr in (arrays or {}).items():
+        a = np.asarray(arr, dtype=np.int64)
+        if a.ndim == 1:
+            a = a[None, :]
+        if name in SUM_ARRAYS:
+            out[name] = a.sum(axis=0)
+        elif name in MAX_ARRAYS:
+            out[name] = a.max(axis=0) if a.shape[0] else np.zeros(a.shape[1], dtype=np.int64)
+        else:
+            raise KeyError(f"unknown statistic {name!r}")
+    return out
+
+
+def _pack(d: Dict[str, np.ndarray], names) -> Tuple[np.ndarray, list]:
+    layout, parts = [], []
+    for name in names:
+        if name in d:
+            a = np.ascontiguousarray(d[name], dtype=np.int64)
+            layout.append((name, a.shape))
+            parts.append(a.reshape(-1))
+    flat = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
+    return flat, layout
+
+
+def _unpack(flat: np.ndarray, layout) -> Dict[str, np.ndarray]:
+    out, pos = {}, 0
+    for name, shape in layout:
+        size = int(np.prod(shape))
+        out[name] = flat[pos:pos + size].reshape(shape)
+        pos += size
+    return out
+
+
+def allreduce_statistics(local: Dict[str, np.ndarray], dist=None, device=None) -> Dict[str, np.ndarray]:
+    """Every rank's ``local_statistics`` combined: one SUM all-reduce of the packed additive
+    fields (scalars, histograms, cut_times, num_flips, part_sum) and one MAX all-reduce of
+    last_flipped.  Every rank must pass the same set of fields with the same shapes."""
+    flat_s, lay_s = _pack(local, ("scalars",) + SUM_ARRAYS)
+    flat_m, lay_m = _pack(local, MAX_ARRAYS)
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        import torch
+        t = torch.as_tensor(flat_s, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        flat_s = t.cpu().numpy()
+        if flat_m.size:
+            t = torch.as_tensor(flat_m, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            flat_m = t.cpu().numpy()
+    out = _unpack(flat_s, lay_s)
+    out.update(_unpack(flat_m, lay_m))
+    return out
+
+
+def checksums(red: Dict[str, np.ndarray]) -> Dict[str, int]:
+    """Order-sensitive int64 checksums of the reduced fields (the N > 1 bench line's record of
+    what the collective produced): sum_i (i + 1) * x_i mod 2^63 per field."""
+    out = {}
+    for name, a in red.items():
+        x = np.asarray(a, dtype=np.int64).reshape(-1)
+        w = np.arange(1, x.size + 1, dtype=np.int64)
+        out[name] = int((x * w).sum() & ((1 << 63) - 1))
+    return out

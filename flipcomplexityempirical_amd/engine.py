@@ -117,6 +117,28 @@ class RunConfig:
     recom_epsilon: float = 0.05
     recom_node_repeats: int = 1
     recom_max_attempts: int = 0
+    # launch tuning (fc_params.tune_*): scheduling only, never the trajectory; 0 = default.
+    # Keys: nsub, hit_stop, par_min, wait_queue, chains_per_block, prio_div (3), prio_th (3).
+    tune: Optional[Dict[str, object]] = None
+
+
+TUNE_KEYS = ("nsub", "hit_stop", "par_min", "wait_queue", "chains_per_block", "prio_div", "prio_th")
+
+
+def parse_tune(text: str) -> Dict[str, object]:
+    """``"nsub=2,hit_stop=24,prio_div=2:5:10"`` -> RunConfig.tune (tools / bench.py --tune)."""
+    out: Dict[str, object] = {}
+    for item in filter(None, (t.strip() for t in (text or "").split(","))):
+        key, _, val = item.partition("=")
+        if key not in TUNE_KEYS:
+            raise ValueError(f"unknown tuning key {key!r} (known: {', '.join(TUNE_KEYS)})")
+        if key in ("prio_div", "prio_th"):
+            conv = int if key == "prio_div" else float
+            vals = [conv(x) for x in val.split(":")]
+            out[key] = tuple(vals) + (vals[-1],) * (3 - len(vals)) if len(vals) < 3 else tuple(vals[:3])
+        else:
+            out[key] = int(val)
+    return out
 
 
 class FlipRun:
@@ -158,6 +180,15 @@ class FlipRun:
         prm.recom_epsilon = float(cfg.recom_epsilon)
         prm.recom_node_repeats = int(cfg.recom_node_repeats)
         prm.recom_max_attempts = int(cfg.recom_max_attempts)
+        for key, val in (cfg.tune or {}).items():
+            if key not in TUNE_KEYS:
+                raise ValueError(f"unknown tuning key {key!r}")
+            if key in ("prio_div", "prio_th"):
+                arr = getattr(prm, "tune_" + key)
+                for i, x in enumerate(val):
+                    arr[i] = x
+            else:
+                setattr(prm, "tune_" + key, int(val))
         h = ctypes.c_void_p()
         check(L.fc_run_create(graph.handle, ctypes.byref(prm), self.n_chains, _p(self._init, ctypes.c_int8),
                               _p(self._bases, ctypes.c_double), ctypes.byref(h)), "fc_run_create")

@@ -124,6 +124,24 @@ typedef struct fc_params {
     double recom_epsilon;
     int32_t recom_node_repeats;  /* roots tried per spanning tree (<= 0: 1)                */
     int32_t recom_max_attempts;  /* roots tried per proposal before giving up (<= 0: 10000) */
+    /* Launch tuning.  Scheduling only: no trajectory, statistic or trace depends on these
+     * (tests/test_parity_gpu.py::test_sec11_batch_shapes, test_pair_gpu.py::test_k4_wait_queue_lengths). 0 = the default;
+     * the library reads no environment variables.                                          */
+    int32_t tune_nsub;          /* draw rounds of 64 per batch: k = 2 in {1, 2, 4} (default 4),
+                                   k > 2 in {1, 2} (default 1); anything else FC_ERR_ARG       */
+    int32_t tune_hit_stop;      /* no further draw round once a batch holds this many boundary
+                                   hits (default 32)                                           */
+    int32_t tune_par_min;       /* k = 2: segment-parallel commit from this many acceptances on
+                                   (default 3; > 64 = one event at a time)                     */
+    int32_t tune_wait_queue;    /* accepted states queued for their geometric wait before one
+                                   full-width draw pass (default and maximum: 64 for k = 2, 32
+                                   for k > 2)                                                  */
+    int32_t tune_chains_per_block; /* chains (wavefronts) per workgroup: 1 (default), 2 or 4   */
+    int32_t tune_prio_div[3];   /* k = 2 SIMD issue priority 1/2/3 for chains with |B| below
+                                   n / div (default {2, 5, 10}); tune_prio_div[0] < 0: off      */
+    float tune_prio_th[3];      /* ... and, once a chain has taken 1/16 of the launch's steps,
+                                   for projected finish / previous launch's slowest above these
+                                   (default {0.9, 1.0, 1.1}); tune_prio_th[0] < 0: |B| rule only */
 } fc_params;
 
 /* Per-chain statistics.  "Yields" are the states a `for part in exp_chain` loop sees:

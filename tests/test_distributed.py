@@ -73,3 +73,70 @@ def test_allreduce_world2_gloo():
     for _, tot, mx in res:
         assert np.array_equal(tot, expect)
         assert mx == 2.0
+
+
+# ---- every §8(e) statistic, from real chains of the CPU oracle -------------------------
+N_REAL = 12          # chains of the C1 lattice (10x10 grid), bases cycling over BASES_REAL
+BASES_REAL = (0.5, 1.0, 2.63815853, 4.0)
+STEPS_REAL = 3000
+
+
+def _real_chain(g):
+    """Chain g of the C1 workload on the C oracle with every driver tally on."""
+    from flipcomplexityempirical_amd import graphs as G
+    from oracle.flipref import CRef
+    spec = G.grid_graph(10, 10)
+    a0 = spec.assignment_array(G.threshold_plan(spec.nodes, 0, 5), [-1, 1])
+    _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
+    r = CRef().run(spec, a0, base=BASES_REAL[g % len(BASES_REAL)], pop_lo=lo, pop_hi=hi, seed=77, chain_id=g,
+                   n_steps=STEPS_REAL, log1mp=G.log1mp_table(spec.n, 2), want_hist=True, want_edges=True,
+                   want_flips=True)
+    return r
+
+
+def _real_local(gids):
+    rs = [_real_chain(int(g)) for g in gids]
+    stats = {f: np.asarray([r["stats"][f] for r in rs], dtype=np.int64) for f in D.AGG_FIELDS}
+    arrays = {name: np.stack([r[name] for r in rs]) for name in D.SUM_ARRAYS + D.MAX_ARRAYS}
+    return D.local_statistics(stats, np.asarray(gids) % len(BASES_REAL), len(BASES_REAL), arrays)
+
+
+def _real_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off, cnt = D.shard(N_REAL, world, rank)
+    red = D.allreduce_statistics(_real_local(np.arange(off, off + cnt)), dist)
+    q.put((rank, red, D.checksums(red)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_all_statistics_world2_gloo():
+    """the one reduction carries the |cut| / |B| histograms, per-edge cut_times,
+    per-node num_flips / part_sum (sums) and last_flipped (max) besides the grouped scalars.
+    Real per-chain arrays from the C oracle (C1 lattice, 12 chains over 4 bases) sharded over a
+    gloo world of 2 must reduce to the host-side combination of all 12 chains."""
+    from oracle import flipref
+    flipref.build_lib()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_real_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = _real_local(np.arange(N_REAL))   # every chain on one host, no collective
+    assert set(expect) == {"scalars"} | set(D.SUM_ARRAYS) | set(D.MAX_ARRAYS)
+    rs = [_real_chain(g) for g in range(N_REAL)]
+    assert np.array_equal(expect["cut_times"], sum(r["cut_times"] for r in rs))
+    assert np.array_equal(expect["last_flipped"], np.max([r["last_flipped"] for r in rs], axis=0))
+    # every yield (the initial state + one per step) lands in one |cut| bin
+    assert int(expect["cut_hist"].sum()) == N_REAL * (STEPS_REAL + 1)
+    for _, red, cs in res:
+        for name, arr in expect.items():
+            assert np.array_equal(red[name], arr), name
+        assert cs == D.checksums(expect)

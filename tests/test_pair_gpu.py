@@ -167,3 +167,47 @@ def test_c3_lean_wait_queue(gpu, cref, sec11, launches):
                        trace_cap=0, proposal=1)
         for key in ("steps", "accepted", "sum_wait", "wait_cur", "cut", "nb"):
             assert int(st[key][c]) == int(ref["stats"][key]), (launches[0], c, key)
+
+
+@pytest.mark.parametrize("wait_queue", [1, 2, 7, 32])
+def test_k4_wait_queue_lengths(gpu, cref, sec11, wait_queue):
+    """The deferred-wait queue of the general-k kernel at every length (fc_params
+    tune_wait_queue): a short queue makes batches that accept more states than it holds --
+    the direct-draw path -- the common case, including right after a drain (empty queue) with
+    rejected steps of the batch's start state still to charge (that order once
+    lost wait_cur * r0).  Small bases and a loose population bound make most proposals
+    accepted.  sum_wait and wait_cur are bit-exact against the oracle."""
+    k, n_chains = 4, 16
+    a0 = sec11.assignment_array(G.quadrant_plan(sec11.nodes), list(range(k)))
+    inits = np.stack([a0] * n_chains)
+    bases = np.asarray([[0.1, 0.3, 1.0, G.SEC11_MU][c % 4] for c in range(n_chains)])
+    fg = FlipGraph(sec11)
+    _, (lo, hi) = G.population_bounds(int(sec11.pop.sum()), k, 0.5)
+    cfg = RunConfig(k=k, labels=tuple(range(k)), proposal=_lib.FC_PROPOSE_PAIR, seed=29, pop_lo=lo, pop_hi=hi,
+                    tune={"wait_queue": wait_queue})
+    run = FlipRun(fg, inits, cfg, bases=bases)
+    for n in (3, 40, 700, 1257):
+        run.steps(n)
+    st = run.stats()
+    total = 3 + 40 + 700 + 1257
+    assert int(st["accepted"].sum()) > 0.4 * n_chains * total  # most steps accept: multi-accept batches
+    for c in range(n_chains):
+        ref = cref.run(sec11, inits[c], base=float(bases[c]), pop_lo=lo, pop_hi=hi, seed=29, chain_id=c,
+                       n_steps=total, k=k, labels=list(range(k)), log1mp=G.log1mp_table(sec11.n, k),
+                       trace_cap=0, proposal=1)
+        for key in ("steps", "accepted", "sum_wait", "wait_cur", "sum_cut", "sum_nb", "cut", "nb"):
+            assert int(st[key][c]) == int(ref["stats"][key]), (wait_queue, c, key)
+
+
+def test_tuning_fields_checked(gpu, sec11):
+    """Out-of-range launch tuning is an FC_ERR_ARG (ValueError) naming the field and the kernel,
+    never a generic HIP launch failure (FC_NSUB=4 used to break every k > 2 launch)."""
+    fg = FlipGraph(sec11)
+    a4 = sec11.assignment_array(G.quadrant_plan(sec11.nodes), list(range(4)))
+    _, (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 4, 0.05)
+    base = RunConfig(k=4, labels=tuple(range(4)), proposal=_lib.FC_PROPOSE_PAIR, seed=1, pop_lo=lo, pop_hi=hi)
+    for bad, what in (({"nsub": 4}, "k > 2"), ({"wait_queue": 33}, "tune_wait_queue"),
+                      ({"chains_per_block": 3}, "tune_chains_per_block")):
+        cfg = RunConfig(**{**base.__dict__, "tune": bad})
+        with pytest.raises(ValueError, match=what):
+            FlipRun(fg, a4[None, :], cfg)

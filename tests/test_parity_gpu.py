@@ -160,15 +160,19 @@ def test_sharded_equals_unsharded(gpu, sec11):
         assert np.array_equal(part.state(), fa[off:off + cnt])
 
 
-@pytest.mark.parametrize("nsub,hit_stop", [(1, 64), (2, 32), (4, 12), (4, 32), (4, 64)])
+@pytest.mark.parametrize("nsub,hit_stop,extra", [(1, 64, {}), (2, 32, {}), (4, 12, {}), (4, 32, {}), (4, 64, {}),
+                                               (4, 32, {"wait_queue": 1}), (4, 32, {"wait_queue": 3}),
+                                               (4, 32, {"par_min": 65}), (4, 32, {"par_min": 1}),
+                                               (4, 32, {"chains_per_block": 4}),
+                                               (4, 32, {"prio_div": (-1, 0, 0)}),
+                                               (2, 32, {"prio_th": (-1.0, 0.0, 0.0)})])
 @pytest.mark.parametrize("lean", [True, False])
-def test_sec11_batch_shapes(gpu, cref, sec11, monkeypatch, nsub, hit_stop, lean):
-    """Every compiled draw-round count of the k = 2 kernel (FC_NSUB), the round cut-off
-    (FC_HIT_STOP) and the in-place re-evaluation of stale slots are scheduling choices only:
-    the lean instance (waits only) and the full instance (trace + histograms) stay bit-exact
-    against the oracle under each of them."""
-    monkeypatch.setenv("FC_NSUB", str(nsub))
-    monkeypatch.setenv("FC_HIT_STOP", str(hit_stop))
+def test_sec11_batch_shapes(gpu, cref, sec11, nsub, hit_stop, extra, lean):
+    """Every launch-tuning field of fc_params (draw rounds per batch ``tune_nsub``, the round
+    cut-off ``tune_hit_stop``, the deferred-wait queue length, the segment-parallel threshold,
+    chains per workgroup, issue priorities) is a scheduling choice only: the lean instance
+    (waits only) and the full instance (trace + histograms) stay bit-exact against the oracle
+    under each of them (the guarantee include/flipchain.h states for fc_params.tune_*)."""
     inits, bases = _configs(sec11, G.sec11_plan, G.SEC11_BASES, 30)
     # full: trace + histograms, without the per-edge / per-node tallies, so that stale slot
     # views are re-evaluated in place (the ALL_DIAG tests above cover the batch-ending form)
@@ -176,7 +180,7 @@ def test_sec11_batch_shapes(gpu, cref, sec11, monkeypatch, nsub, hit_stop, lean)
     fg = FlipGraph(sec11)
     (_, _), (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 2, 0.1)
     cfg = RunConfig(seed=11, pop_lo=lo, pop_hi=hi, diag_mask=diag, trace_chains=0 if lean else 30,
-                    trace_cap=0 if lean else 200000)
+                    trace_cap=0 if lean else 200000, tune=dict(nsub=nsub, hit_stop=hit_stop, **extra))
     run = FlipRun(fg, inits, cfg, bases=bases)
     run.steps(1500)
     run.steps(1500)

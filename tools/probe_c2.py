@@ -3,7 +3,7 @@ import sys, time, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 from flipcomplexityempirical_amd import graphs as G, _lib
-from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune
 spec = G.sec11_graph(); fg = FlipGraph(spec)
 C = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
@@ -14,7 +14,7 @@ inits = np.stack([plans[(c // 10) % 3] for c in range(C)])
 bases = np.asarray([G.SEC11_BASES[c % 10 if B < 0 else B] for c in range(C)])
 (_, _), (lo, hi) = G.population_bounds(1596, 2, 0.1)
 # FC_PROBE_DIAG=<mask> overrides the diagnostics mask (0: no geometric waits)
-cfg = RunConfig(seed=0x5EED0002, pop_lo=lo, pop_hi=hi)
+cfg = RunConfig(seed=0x5EED0002, pop_lo=lo, pop_hi=hi, tune=parse_tune(os.environ.get('FC_TUNE', '')))
 if 'FC_PROBE_DIAG' in os.environ: cfg.diag_mask = int(os.environ['FC_PROBE_DIAG'])
 run = FlipRun(fg, inits, cfg, bases=bases)
 for it in range(IT):

@@ -8,7 +8,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import bench
 from flipcomplexityempirical_amd import graphs as G
-from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune
 
 W = bench.Workload(sys.argv[1])
 C = int(sys.argv[2]) if len(sys.argv) > 2 else W.chains
@@ -18,7 +18,7 @@ fg = FlipGraph(W.spec)
 inits = np.stack([W.init_of(g) for g in range(C)])
 bases = np.asarray([W.base_of(g) for g in range(C)])
 _, (lo, hi) = G.population_bounds(int(W.spec.pop.sum()), W.k, W.pct)
-run = FlipRun(fg, inits, RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo,
+run = FlipRun(fg, inits, RunConfig(tune=parse_tune(os.environ.get('FC_TUNE', '')), k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo,
                                    pop_hi=hi), bases=bases)
 for it in range(IT):
     s0 = run.stats()
