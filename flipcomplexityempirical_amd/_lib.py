@@ -28,7 +28,7 @@ FC_CON_CONTIG, FC_CON_POP, FC_CON_BOUNDARY, FC_CON_FIXED, FC_CON_EMPTY = 0x1, 0x
 
 EXPORTED = [
     "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
-    "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
+    "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_set_initial_wait", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
     "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_read_recom_trace",
     "fc_run_trace_reset", "fc_run_read_hist",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
@@ -125,6 +125,7 @@ def load(build_if_missing: bool = True):
     L.fc_run_create.argtypes = [vp, _P(Params), i32, _P(ctypes.c_int8), _P(dbl), _P(vp)]
     L.fc_run_steps.argtypes = [vp, i64, i64, vp]
     L.fc_run_set_tape.argtypes = [vp, _P(ctypes.c_uint32), i64]
+    L.fc_run_set_initial_wait.argtypes = [vp, _P(ctypes.c_uint32)]
     L.fc_run_sync.argtypes = [vp]
     L.fc_run_last_ms.argtypes = [vp, _P(ctypes.c_float)]
     L.fc_run_timings.argtypes = [vp, _P(ctypes.c_float), i32, _P(i32)]

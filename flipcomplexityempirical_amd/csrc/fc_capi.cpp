@@ -541,6 +541,25 @@ int fc_run_set_tape(fc_run *r, const uint32_t *tape, int64_t n_draws) {
     return FC_OK;
 }
 
+int fc_run_set_initial_wait(fc_run *r, const uint32_t *words) {
+    if (!r || !words) return fail(FC_ERR_ARG, "fc_run_set_initial_wait: null argument");
+    if (!(r->p.diag_mask & FC_DIAG_WAIT)) return fail(FC_ERR_ARG, "fc_run_set_initial_wait: FC_DIAG_WAIT is off");
+    if (r->p.proposal == FC_PROPOSE_RECOM) return fail(FC_ERR_UNSUPPORTED, "fc_run_set_initial_wait: flip runs only");
+    if (int rc = fc_run_sync(r)) return rc;
+    std::vector<fc::ChainScalars> sc(r->n_chains);
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    for (const auto &s : sc)
+        if (s.steps != 0 || s.draw != 0) return fail(FC_ERR_ARG, "fc_run_set_initial_wait: a chain has stepped");
+    for (int32_t c = 0; c < r->n_chains; ++c) {
+        fc::ChainScalars &s = sc[c];
+        const int64_t w = fc::geom_from(fc::u53(words[2 * c], words[2 * c + 1]), r->log1mp[s.nb]);
+        s.sum_wait += w - s.wait_cur;  // yield #0's term
+        s.wait_cur = w;
+    }
+    HIP_TRY(hipMemcpy(r->d_sc, sc.data(), sc.size() * sizeof(sc[0]), hipMemcpyHostToDevice));
+    return FC_OK;
+}
+
 int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream) {
     if (!r) return fail(FC_ERR_ARG, "fc_run_steps: null run");
     if (n_steps < 0) return fail(FC_ERR_ARG, "fc_run_steps: n_steps must be >= 0");

@@ -59,11 +59,17 @@ bool check_planar(const HostGraph &g) {
     for (int32_t e = 0; e < E; ++e)
         len += std::hypot(g.pos[2 * g.eu[e]] - g.pos[2 * g.ev[e]], g.pos[2 * g.eu[e] + 1] - g.pos[2 * g.ev[e] + 1]);
     double cell = std::max(len / E, 1e-9);
-    int64_t nx = std::min<int64_t>(4096, (int64_t)((maxx - minx) / cell) + 1);
-    int64_t ny = std::min<int64_t>(4096, (int64_t)((maxy - miny) / cell) + 1);
+    if (!std::isfinite(cell)) cell = 1e300;  // positions near DBL_MAX: one bucket, still exact
+    // bucket coordinates are clamped in double before any integer conversion (a far-out or
+    // overflowing ratio would otherwise be an undefined float -> int64 cast)
+    auto bucket = [](double t, int64_t hi) -> int64_t {
+        if (!(t > 0.0)) return 0;
+        return t >= (double)(hi - 1) ? hi - 1 : (int64_t)t;
+    };
+    const int64_t nx = bucket((maxx - minx) / cell, 4096) + 1, ny = bucket((maxy - miny) / cell, 4096) + 1;
     std::unordered_map<int64_t, std::vector<int32_t>> buckets;
-    auto cx = [&](double x) { return std::min<int64_t>(nx - 1, std::max<int64_t>(0, (int64_t)((x - minx) / cell))); };
-    auto cy = [&](double y) { return std::min<int64_t>(ny - 1, std::max<int64_t>(0, (int64_t)((y - miny) / cell))); };
+    auto cx = [&](double x) { return bucket((x - minx) / cell, nx); };
+    auto cy = [&](double y) { return bucket((y - miny) / cell, ny); };
     for (int32_t e = 0; e < E; ++e) {
         const double *a = &g.pos[2 * g.eu[e]], *b = &g.pos[2 * g.ev[e]];
         for (int64_t x = cx(std::min(a[0], b[0])); x <= cx(std::max(a[0], b[0])); ++x)
@@ -148,6 +154,8 @@ std::string build_host_graph(int32_t n, const int32_t *row_ptr, const int32_t *c
     std::vector<uint8_t> exact(n, 0), gamma(n, 0);
 
     if (pos_xy) {
+        for (size_t i = 0; i < 2 * (size_t)n; ++i)
+            if (!std::isfinite(pos_xy[i])) return "graph: node positions must be finite";
         g.pos.assign(pos_xy, pos_xy + 2 * (size_t)n);
         g.planar = check_planar(g);
         // ccw neighbour order

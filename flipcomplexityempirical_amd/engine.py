@@ -212,6 +212,12 @@ class FlipRun:
         self._tape = t
         check(_lib.load().fc_run_set_tape(self.handle, _p(t, ctypes.c_uint32), n_draws), "fc_run_set_tape")
 
+    def set_initial_wait(self, words: np.ndarray):
+        """Replay the initial states' geometric waits: ``words`` is ``[n_chains, 2]`` u32 (the
+        53-bit uniform numpy's geometric inverted; ``fc_run_set_initial_wait``)."""
+        w = np.ascontiguousarray(words, dtype=np.uint32).reshape(self.n_chains, 2)
+        check(_lib.load().fc_run_set_initial_wait(self.handle, _p(w, ctypes.c_uint32)), "fc_run_set_initial_wait")
+
     def sync(self):
         check(_lib.load().fc_run_sync(self.handle))
 

@@ -231,6 +231,13 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
 /* Replay mode: chain c reads its random words from tape[c * n_draws * 6 ...] (6 u32 per
  * draw: 4 proposal words, 2 geometric words) instead of Philox.  NULL detaches. */
 int fc_run_set_tape(fc_run *r, const uint32_t *tape, int64_t n_draws);
+/* Replay of the initial state's geometric wait (geom_wait :147-148, drawn by numpy for the
+ * yielded initial state in the reference): chain c's wait becomes the inversion of the 53-bit
+ * uniform in words[2c], words[2c + 1] (same layout as tape words 4-5) instead of the
+ * purpose-2 Philox draw.  Together with a node tape this replays a
+ * trajectory of the reference's own random streams bit for bit.  Only before the first
+ * fc_run_steps (FC_ERR_ARG after); needs FC_DIAG_WAIT.                                     */
+int fc_run_set_initial_wait(fc_run *r, const uint32_t *words);
 int fc_run_sync(fc_run *r);
 /* Device time of the last fc_run_steps launch, from HIP events on its stream. */
 int fc_run_last_ms(fc_run *r, float *ms);

@@ -74,26 +74,28 @@ static int flip_contiguous_ctx(ctx_t *c, int32_t v) {
     if (n_old == 1) return 1;
     if (++c->stamp_id == 0x7fffffff) { memset(c->stamp, 0, sizeof(int32_t) * (size_t)p->n); c->stamp_id = 1; }
     const int32_t sid = c->stamp_id;
-    int32_t head = 0, tail = 0, found = 1;
+    int32_t head = 0, tail = 0, reached = 0;
     c->stamp[v] = sid;       /* v is removed from the district */
     c->stamp[start] = sid;
     c->queue[tail++] = start;
-    /* count targets reached */
+    /* BFS over A - v from one old neighbour; a dequeued node adjacent to v is an old
+       neighbour reached.  All reached <=> every old neighbour is connected to `start`
+       (the Dijkstra calls of single_flip_contiguous [gc-0.2] ask exactly this), so the
+       search may stop there; otherwise it exhausts start's component. */
     while (head < tail) {
         int32_t u = c->queue[head++];
         for (int32_t j = p->row_ptr[u]; j < p->row_ptr[u + 1]; ++j) {
             int32_t w = p->col_idx[j];
+            if (w == v) {
+                if (++reached == n_old) return 1;
+                continue;
+            }
             if (c->a[w] != A || c->stamp[w] == sid) continue;
             c->stamp[w] = sid;
             c->queue[tail++] = w;
         }
     }
-    found = 0;
-    for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) {
-        int32_t w = p->col_idx[j];
-        if (c->a[w] == A && c->stamp[w] == sid) ++found;
-    }
-    return found == n_old;
+    return 0;
 }
 
 int fr_flip_contiguous(int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
@@ -137,7 +139,11 @@ int fr_districts_contiguous(int32_t n, const int32_t *row_ptr, const int32_t *co
 }
 
 static void draw_words(const fr_params *p, int64_t d, uint32_t purpose, uint32_t w[4]) {
-    if (p->tape && purpose != 2) {   /* the initial state's wait always comes from Philox */
+    if (purpose == 2 && p->wait0_words) {  /* replayed initial-state wait */
+        w[0] = p->wait0_words[0]; w[1] = p->wait0_words[1]; w[2] = 0; w[3] = 0;
+        return;
+    }
+    if (p->tape && purpose != 2) {   /* a tape's initial-state wait is Philox unless wait0_words */
         const uint32_t *t = p->tape + 6 * d;
         if (purpose == 0) { w[0] = t[0]; w[1] = t[1]; w[2] = t[2]; w[3] = t[3]; }
         else { w[0] = t[4]; w[1] = t[5]; w[2] = 0; w[3] = 0; }

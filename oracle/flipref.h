@@ -89,6 +89,9 @@ typedef struct fr_params {
     const uint8_t *boundary;   /* [n] boundary_node flags (boundary_condition)     */
     const int32_t *pinned;     /* [2 n_pinned] edges fixed_endpoints keeps cut     */
     int32_t n_pinned;
+    /* node-tape replay: the two words of the initial state's geometric
+     * wait (numpy's draw in the reference, geom_wait :147-148); NULL = Philox purpose 2   */
+    const uint32_t *wait0_words;
 } fr_params;
 
 #define FR_ACCEPT_CUT 0        /* cut_accept                          :171-179 */

@@ -112,7 +112,7 @@ class FrParams(ctypes.Structure):
                 ("log1mp", _P(ctypes.c_double)), ("proposal", ctypes.c_int32), ("wmax", ctypes.c_int32),
                 ("accept", ctypes.c_int32), ("con_valid", ctypes.c_uint32), ("con_accept", ctypes.c_uint32),
                 ("beta", ctypes.c_double), ("boundary", _P(ctypes.c_uint8)), ("pinned", _P(ctypes.c_int32)),
-                ("n_pinned", ctypes.c_int32)]
+                ("n_pinned", ctypes.c_int32), ("wait0_words", _P(ctypes.c_uint32))]
 
 
 ACCEPT_CUT, ACCEPT_UNIFORM, ACCEPT_ANNEAL = 0, 1, 2
@@ -184,7 +184,8 @@ class CRef:
             max_draws: int = 0, trace_cap: int = 0, want_hist: bool = False,
             want_edges: bool = False, want_flips: bool = False, proposal: int = 0, wmax: int = 0,
             accept: int = 0, con_valid: int = 0, con_accept: int = 0, beta: float = 0.0,
-            boundary: Optional[np.ndarray] = None, pinned: Optional[np.ndarray] = None) -> Dict:
+            boundary: Optional[np.ndarray] = None, pinned: Optional[np.ndarray] = None,
+            wait0_words: Optional[np.ndarray] = None) -> Dict:
         n, E = spec.n, spec.n_edges
         row_ptr = np.ascontiguousarray(spec.row_ptr, dtype=np.int32)
         col_idx = np.ascontiguousarray(spec.col_idx, dtype=np.int32)
@@ -197,6 +198,7 @@ class CRef:
         tp = None if tape is None else np.ascontiguousarray(tape, dtype=np.uint32)
         bnd = None if boundary is None else np.ascontiguousarray(boundary, dtype=np.uint8)
         pin = None if pinned is None else np.ascontiguousarray(pinned, dtype=np.int32).reshape(-1)
+        w0 = None if wait0_words is None else np.ascontiguousarray(wait0_words, dtype=np.uint32).reshape(2)
         p = FrParams(n=n, row_ptr=_ptr(row_ptr, ctypes.c_int32), col_idx=_ptr(col_idx, ctypes.c_int32),
                      pop=_ptr(pop, ctypes.c_int32), k=k, labels=_ptr(lab, ctypes.c_int32),
                      base=float(base), pop_lo=int(pop_lo), pop_hi=int(pop_hi), seed=int(seed),
@@ -205,7 +207,8 @@ class CRef:
                      n_steps=int(n_steps), max_draws=int(max_draws), log1mp=_ptr(l1, ctypes.c_double),
                      proposal=int(proposal), wmax=int(wmax), accept=int(accept), con_valid=int(con_valid),
                      con_accept=int(con_accept), beta=float(beta), boundary=_ptr(bnd, ctypes.c_uint8),
-                     pinned=_ptr(pin, ctypes.c_int32), n_pinned=0 if pin is None else pin.size // 2)
+                     pinned=_ptr(pin, ctypes.c_int32), n_pinned=0 if pin is None else pin.size // 2,
+                     wait0_words=_ptr(w0, ctypes.c_uint32))
         trace = np.zeros(trace_cap, dtype=RECORD_DTYPE) if trace_cap else None
         final = np.zeros(n, dtype=np.int8)
         cut_hist = np.zeros(E + 1, dtype=np.int64) if want_hist else None
@@ -473,29 +476,72 @@ class NativeRngChain(GcFaithfulChain):
     ``random.random()`` in cut_accept (:179), ``np.random.geometric`` in geom_wait (:148),
     and the ``random.choice`` that gerrychain's single_flip_contiguous makes among the old
     neighbours [gc-0.2] -- CPython's Mersenne Twister and numpy's legacy RandomState,
-    seeded per chain instead of globally."""
+    seeded per chain instead of globally.
+
+    ``record=True`` also writes the **node tape** of SURVEY App. A.4: per proposal, the six
+    words the device / C oracle replay (``fc_run_set_tape``) -- word 0 maps to the drawn node
+    under the exact Lemire map, words 1-2 carry the 53-bit ``random()`` value of a valid
+    proposal, words 4-5 the 53-bit ``random_sample()`` numpy's geometric inverted for the
+    state it created -- plus the initial state's wait words (``fc_run_set_initial_wait``)
+    and the per-proposal trace in the device's record layout.  Every draw of this chain is a
+    proposal (it samples B itself), so tape draw i is proposal i."""
 
     def __init__(self, spec, plan: Dict, *, base: float, pop_bounds, seed: int,
-                 log1mp: Optional[np.ndarray] = None):
+                 log1mp: Optional[np.ndarray] = None, record: bool = False):
         import random as _random
         self.rng = _random.Random(seed)
         self.nprng = np.random.RandomState(seed & 0xFFFFFFFF)
+        self.record = record
+        self.tape_words = []      # 6 u32 per proposal
+        self.wait0_words = None
+        self._geom_words = None   # words of the last geometric draw
         super().__init__(spec, plan, base=base, pop_bounds=pop_bounds, seed=seed, chain_id=0, log1mp=log1mp)
+        if record:
+            self.wait0_words = self._geom_words
+
+    @staticmethod
+    def _u53_words(u: float):
+        """(a, b) with ((a >> 5) * 2^26 + (b >> 6)) / 2^53 == u (CPython random(), numpy
+        random_sample()): the exact inverse of u53 for any 53-bit double in [0, 1)."""
+        x = int(u * 9007199254740992.0)
+        assert x / 9007199254740992.0 == u
+        return (x >> 26) << 5, (x & ((1 << 26) - 1)) << 6
+
+    def _node_word(self, v: int) -> int:
+        """x0 with (x0 * N) >> 32 == v and (x0 * N) mod 2^32 >= 2^32 mod N (never rejected)."""
+        N = self.n
+        x0 = (((v + 1) << 32) - 1) // N
+        m = x0 * N
+        assert m >> 32 == v and (m & 0xFFFFFFFF) >= (1 << 32) % N
+        return x0
 
     def _geom(self, d, purpose):
         if self.log1mp is None:
             return 0
         s = self.state
         p = len(list(s["b_nodes"])) / (len(self.g.nodes) ** len(self.labels) - 1)  # :148
-        return int(self.nprng.geometric(p, 1)[0]) - 1
+        if self.record:
+            clone = np.random.RandomState()
+            clone.set_state(self.nprng.get_state())
+            U = clone.random_sample()
+            self._geom_words = self._u53_words(U)
+        w = int(self.nprng.geometric(p, 1)[0]) - 1
+        if self.record:  # the replayed inversion must give numpy's own answer
+            nb = len(s["b_nodes"])
+            q = math.log(1.0 - U) / float(self.log1mp[nb])
+            assert int(math.ceil(q)) - 1 == w, (U, p, w)
+        return w
 
     def step(self):
         while True:
             s = self.state
             node = self.rng.choice(list(s["b_nodes"]))  # :143
+            draw = self.stats["draws"]
             self.stats["draws"] += 1
             self.stats["proposals"] += 1
             target = -1 * s.assignment[node]  # :145
+            tid = self.labels.index(target) << 8
+            words = [self._node_word(self.spec.index[node]), 0, 0, 0, 0, 0] if self.record else None
             proposal = s.flip({node: target})
             s.parent = None
             old_nbrs = [nd for nd in self.g.neighbors(node) if proposal.assignment[nd] == s.assignment[node]]
@@ -504,15 +550,38 @@ class NativeRngChain(GcFaithfulChain):
             bad = self._valid(proposal)
             if bad:
                 self.stats["inv_contig" if bad == FLAG_INV_CONTIG else "inv_pop"] += 1
+                if self.record:
+                    self.tape_words.extend(words)
+                    self.trace.append((draw, self.spec.index[node], bad | tid, len(s["cut_edges"]),
+                                       len(s["b_nodes"]), 0))
                 continue
             self.stats["steps"] += 1
             bound = self.base ** (-len(proposal["cut_edges"]) + len(s["cut_edges"]))  # :175
-            if self.rng.random() < bound:  # :179
+            u = self.rng.random()
+            acc = u < bound  # :179
+            if self.record:
+                words[1], words[2] = self._u53_words(u)
+            if acc:
                 self.state = proposal
                 self.stats["accepted"] += 1
                 self.wait = self._geom(0, 1)
+                if self.record:
+                    words[4], words[5] = self._geom_words
             self._yield()
+            if self.record:
+                self.tape_words.extend(words)
+                cur = self.state
+                self.trace.append((draw, self.spec.index[node], FLAG_VALID | (FLAG_ACCEPTED if acc else 0) | tid,
+                                   len(cur["cut_edges"]), len(cur["b_nodes"]), self.wait))
             return self.state
+
+    def node_tape(self) -> np.ndarray:
+        """The recorded node tape, ``[proposals * 6]`` u32."""
+        return np.asarray(self.tape_words, dtype=np.uint32)
+
+    def trace_array(self) -> np.ndarray:
+        return np.asarray(self.trace, dtype=[("draw", "<i8"), ("v", "<i4"), ("flags", "<i4"), ("cut", "<i4"),
+                                             ("nb", "<i4"), ("wait", "<i8")])
 
 
 # --------------------------------------------------------------------------------------

@@ -7,7 +7,10 @@ native_rng_c1.npz: config C1 of BASELINE.json: 10x10 grid, k = 2, plan x[0] >= 5
 tolerance 0.1, bases 1 and mu = 2.63815853 (grid_chain_sec11.py:33); 400 chains per base,
 T = 2000 steps each, chain i seeded 1000 + i.
 native_rng_sec11.npz: the sec11 lattice of the headline (grid_chain_sec11.py:186-260),
-alignment-2 plan, pop tolerance 0.1, bases 0.8 and mu; 200 chains per base, T = 1000 steps.
+alignment-2 plan, pop tolerance 0.1, bases 0.8 and mu; 200 chains per base, T = 1000 steps;
+plus the district-shape statistics of the driver's slope / angle lines (:371-394): each
+chain's mean angle over the yields with exactly two frame cut edges, the end state's angle,
+and the fraction of such yields.
 Run: python tests/golden/make_native.py  (about 1.5 min on 8 cores)."""
 import os
 import sys
@@ -21,10 +24,25 @@ sys.path.insert(0, ROOT)
 CONFIGS = {"c1": ([1.0, 2.63815853], 400, 2000), "sec11": ([0.8, 2.63815853], 200, 1000)}
 
 
+SHAPE = ("angle_mean", "angle_end", "frame2_frac")  # sec11 only (the reference's frame)
+
+
+def _frame_angle(state, frame_edges):
+    """The driver's shape lines (grid_chain_sec11.py:371-394) on the reference's own
+    ``boundary_slope`` filter (:55-78): (number of frame cut edges, angle when exactly two --
+    the only case whose value does not depend on CPython's set order)."""
+    from oracle.flipref import slope_angle
+    a = state.assignment
+    cut = [e for e in frame_edges if a[e[0]] != a[e[1]]]
+    if len(cut) != 2:
+        return len(cut), float("nan")
+    return 2, slope_angle(cut)[1]
+
+
 def one(args):
     cfg, base, i, T = args
     from flipcomplexityempirical_amd import graphs as G
-    from oracle.flipref import NativeRngChain
+    from oracle.flipref import NativeRngChain, boundary_slope
     if cfg == "c1":
         spec = G.grid_graph(10, 10)
         plan = G.threshold_plan(spec.nodes, 0, 5)
@@ -33,10 +51,26 @@ def one(args):
         plan = G.sec11_plan(2, spec.nodes)
     (lo, hi), _ = G.population_bounds(spec.n, 2, 0.1)
     ch = NativeRngChain(spec, plan, base=base, pop_bounds=(lo, hi), seed=1000 + i, log1mp=G.log1mp_table(spec.n, 2))
-    ch.run(T)
+    shape = ()
+    if cfg == "c1":
+        ch.run(T)
+    else:
+        # every edge boundary_slope can return (its filter over all edges), then per yield
+        frame = boundary_slope({tuple(sorted(e)) for e in spec.nx_graph.edges})
+        n2, ang = _frame_angle(ch.state, frame)
+        ang_sum, n_two = (ang if n2 == 2 else 0.0), int(n2 == 2)
+        for _ in range(T):
+            acc0 = ch.stats["accepted"]
+            ch.step()
+            if ch.stats["accepted"] != acc0:
+                n2, ang = _frame_angle(ch.state, frame)
+            if n2 == 2:
+                ang_sum += ang
+                n_two += 1
+        shape = (ang_sum / n_two if n_two else float("nan"), ang if n2 == 2 else float("nan"), n_two / (T + 1))
     s = ch.state
     return (len(s["cut_edges"]), len(s["b_nodes"]), s["population"][1], ch.wait,
-            ch.stats["sum_cut"] / (T + 1), ch.stats["sum_nb"] / (T + 1))
+            ch.stats["sum_cut"] / (T + 1), ch.stats["sum_nb"] / (T + 1)) + shape
 
 
 def main(which=None):
@@ -47,7 +81,8 @@ def main(which=None):
         with ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
             for bi, b in enumerate(bases):
                 r = np.asarray(list(ex.map(one, [(cfg, b, i, T) for i in range(M)])), dtype=np.float64)
-                for j, name in enumerate(("cut", "nb", "pop1", "wait", "mean_cut", "mean_nb")):
+                names = ("cut", "nb", "pop1", "wait", "mean_cut", "mean_nb") + (SHAPE if cfg == "sec11" else ())
+                for j, name in enumerate(names):
                     out[f"b{bi}_{name}"] = r[:, j]
         np.savez_compressed(os.path.join(os.path.dirname(os.path.abspath(__file__)), f"native_rng_{cfg}.npz"), **out)
 

@@ -9,8 +9,12 @@ tests/golden/make_native.py) against the canonical Philox stream of the C oracle
   sec11: the headline lattice (grid_chain_sec11.py:186-260), alignment-2 plan, pop
          tolerance 0.1, bases 0.8 and mu, 1000 steps.
 Two-sample KS tests on the end state's |cut edges|, |b_nodes| and district population, each
-chain's time-averaged |cut| and |B|, and the geometric wait of the end state.  The device is
-held to the same fixtures in tests/test_distribution_gpu.py.
+chain's time-averaged |cut| and |B|, and the geometric wait of the end state; for sec11 also
+the district-shape statistics of the driver's slope / angle lines (grid_chain_sec11.py:55-78,
+371-394): each chain's mean interface angle over its yields and the end state's angle (with
+both districts contiguous exactly two frame edges are cut, so the angle does not depend on
+the reference's set order).  The device is held to the same fixtures in
+tests/test_distribution_gpu.py, with the angles from its own frame-series kernel.
 """
 import os
 
@@ -22,6 +26,7 @@ from flipcomplexityempirical_amd import graphs as G
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 STATS = ("cut", "nb", "pop1", "wait", "mean_cut", "mean_nb")
+SHAPE_STATS = ("angle_mean", "angle_end")  # sec11 only
 P_MIN = 1e-3  # per comparison; the samples are fixed (seeded), so the outcome is deterministic
 CASES = [("c1", 0), ("c1", 1), ("sec11", 0), ("sec11", 1)]
 
@@ -54,10 +59,41 @@ def summarize(spec, finals, waits, sum_cut, sum_nb, T):
 
 
 def assert_same_distribution(fix, bi, got, label):
-    for s in STATS:
+    names = STATS + tuple(s for s in SHAPE_STATS if s in got)
+    if f"b{bi}_angle_mean" in fix.files:
+        assert all(s in got for s in SHAPE_STATS), "shape statistics missing"
+    for s in names:
         ref = fix[f"b{bi}_{s}"]
-        p = ks_2samp(ref, got[s]).pvalue
-        assert p > P_MIN, (label, s, p, ref.mean(), got[s].mean())
+        ref, val = ref[np.isfinite(ref)], np.asarray(got[s], float)
+        val = val[np.isfinite(val)]
+        p = ks_2samp(ref, val).pvalue
+        assert p > P_MIN, (label, s, p, ref.mean(), val.mean())
+
+
+def angle_of(mid_a, mid_b, center=(20.0, 20.0)):
+    """The driver's angle line (:391-394) on two frame-edge midpoints."""
+    anga = np.asarray(mid_a, float) - center
+    angb = np.asarray(mid_b, float) - center
+    return float(np.arccos(np.clip(np.dot(anga / np.linalg.norm(anga), angb / np.linalg.norm(angb)), -1, 1)))
+
+
+def shape_from_events(spec, frame, a0, events, T):
+    """(mean angle over the yields with exactly two frame cut edges, end angle) of one chain
+    from its accepted flips ``events`` = [(t, v)] (t = the yield the flip creates)."""
+    a = a0.copy()
+    def state():
+        m = np.nonzero(a[frame.eu] != a[frame.ev])[0]
+        return (angle_of(frame.mid[m[0]], frame.mid[m[1]]) if m.size == 2 else np.nan)
+    vals, ts = [state()], [0]
+    for t, v in events:
+        a[v] = 1 - a[v]
+        vals.append(state())
+        ts.append(int(t))
+    w = np.diff(np.asarray(ts + [T + 1]))
+    vals = np.asarray(vals)
+    ok = np.isfinite(vals)
+    mean = float(np.sum(vals[ok] * w[ok]) / np.sum(w[ok])) if ok.any() else np.nan
+    return mean, vals[-1]
 
 
 @pytest.mark.parametrize("cfg,bi", CASES)
@@ -65,12 +101,23 @@ def test_canonical_oracle_matches_native_rng(cref, cfg, bi):
     fix = fixture(cfg)
     T, base = int(fix["T"]), float(fix["bases"][bi])
     spec, a0, lo, hi = setup(cfg)
-    finals, waits, sc, sn = [], [], [], []
+    from oracle.flipref import events_from_trace
+    frame = G.slope_frame(spec, "sec11") if cfg == "sec11" else None
+    finals, waits, sc, sn, am, ae = [], [], [], [], [], []
     for c in range(600):
         r = cref.run(spec, a0, base=base, pop_lo=lo, pop_hi=hi, seed=0xD15, chain_id=c, n_steps=T,
-                     log1mp=G.log1mp_table(spec.n, 2))
+                     log1mp=G.log1mp_table(spec.n, 2), trace_cap=64 * T if frame is not None else 0)
         finals.append(r["final"])
         waits.append(r["stats"]["wait_cur"])
         sc.append(r["stats"]["sum_cut"])
         sn.append(r["stats"]["sum_nb"])
-    assert_same_distribution(fix, bi, summarize(spec, finals, waits, sc, sn, T), f"C oracle {cfg}")
+        if frame is not None:
+            assert len(r["trace"]) < 64 * T
+            ev = events_from_trace(r["trace"])
+            m, e = shape_from_events(spec, frame, a0, ev[:, :2], T)
+            am.append(m)
+            ae.append(e)
+    got = summarize(spec, finals, waits, sc, sn, T)
+    if frame is not None:
+        got["angle_mean"], got["angle_end"] = np.asarray(am), np.asarray(ae)
+    assert_same_distribution(fix, bi, got, f"C oracle {cfg}")

@@ -5,6 +5,7 @@ import pytest
 
 from flipcomplexityempirical_amd import _lib
 from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+from flipcomplexityempirical_amd import graphs as G
 from tests.test_distribution import CASES, assert_same_distribution, fixture, setup, summarize
 
 pytestmark = pytest.mark.gpu
@@ -16,9 +17,28 @@ def test_device_matches_native_rng(gpu, cfg, bi):
     T, base = int(fix["T"]), float(fix["bases"][bi])
     spec, a0, lo, hi = setup(cfg)
     C = 4096
+    shape = cfg == "sec11"
+    diag = _lib.FC_DIAG_WAIT | (_lib.FC_DIAG_SERIES if shape else 0)
     run = FlipRun(FlipGraph(spec), np.stack([a0] * C),
-                  RunConfig(seed=0xD15C0 + bi, pop_lo=lo, pop_hi=hi, base=base, diag_mask=_lib.FC_DIAG_WAIT))
+                  RunConfig(seed=0xD15C0 + bi, pop_lo=lo, pop_hi=hi, base=base, diag_mask=diag,
+                            event_cap=T + 1 if shape else 0))
     run.steps(T)
     st, fin = run.stats(), run.state()
     got = summarize(spec, fin, st["wait_cur"], st["sum_cut"], st["sum_nb"], T)
+    if shape:
+        # the interface angle after every accepted flip, from the device's frame-series kernel
+        # (fc_run_frame_series: boundary_slope + the driver's angle line), weighted by the
+        # yields each state lasts
+        fs = run.frame_series(G.slope_frame(spec, "sec11"))
+        am, ae = np.full(C, np.nan), np.full(C, np.nan)
+        for c in range(C):
+            ev = run.events(c)
+            n = int(fs["len"][c])
+            assert n == ev.size + 1
+            w = np.diff(np.concatenate([[0], ev["t"], [T + 1]]))
+            ang, two = fs["angle"][c, :n], fs["n_cut"][c, :n] == 2
+            if two.any():
+                am[c] = float(np.sum(ang[two] * w[two]) / np.sum(w[two]))
+            ae[c] = ang[-1] if two[-1] else np.nan
+        got["angle_mean"], got["angle_end"] = am, ae
     assert_same_distribution(fix, bi, got, f"device {cfg}")

@@ -9,8 +9,10 @@ decoded ``*end2.png`` final states and the ``*wait.txt`` sums.  Pins:
    oracle's checkers -- states the reference's chain actually reached;
 3. ``single_flip_contiguous`` restated (BFS) agrees with the device's planar local rule on
    every boundary node of every decoded state (the exactness claim of DESIGN.md);
-4. the oracle chain reproduces the reference's ``wait.txt`` sums per base (100,000 yields,
-   same graphs / plans / bounds / bases) within the reference's own run-to-run spread.
+4. the oracle chain, re-run on all 174 reference configurations (every base x pop x
+   alignment of both sweeps), reproduces the reference's ``wait.txt`` sums per (base, pop)
+   and per base, and its final |cut| / |B| distributions per base match the decoded end
+   states (``tests/reference_pin.py``).
 """
 import os
 import re
@@ -129,35 +131,28 @@ def test_local_rule_exact_on_reference_states(gold, cref, sec11, frank):
     assert checked > 10000
 
 
-def _one_run(args):
-    graph, al, base, pct, seed = args
+def _pin_run(args):
+    (tag, al, base, pct, key), seed = args
     from oracle.flipref import CRef
-    spec = G.sec11_graph() if graph == "sec11" else G.frank_graph()
-    plan = (G.sec11_plan if graph == "sec11" else G.frank_plan)(al, spec.nodes)
-    a0 = spec.assignment_array(plan, [-1, 1])
+    import reference_pin as RP
+    spec = RP.spec_of(tag)
     _, (lo, hi) = G.population_bounds(spec.n, 2, pct)
-    r = CRef().run(spec, a0, base=base, pop_lo=lo, pop_hi=hi, seed=seed, chain_id=al, n_steps=99999,
-                   log1mp=G.log1mp_table(spec.n, 2))
-    return r["stats"]["sum_wait"], r["stats"]["cut"]
+    r = CRef().run(spec, RP.start_plan(spec, tag, al), base=base, pop_lo=lo, pop_hi=hi, seed=seed, chain_id=al,
+                   n_steps=99999, log1mp=G.log1mp_table(spec.n, 2))
+    return r["stats"]["sum_wait"], r["stats"]["cut"], r["stats"]["nb"]
 
 
-def test_oracle_reproduces_reference_wait_sums(gold):
-    """total_steps = 100000 yields (grid_chain_sec11.py:342) -> 99999 steps after S0."""
-    jobs, groups = [], []
-    for tag, bases in (("sec11", G.SEC11_BASES), ("frank", G.FRANK_BASES)):
-        for base in bases:
-            for al in range(3):
-                jobs.append((tag, al, base, 0.5, 1000 + al))
-                groups.append((tag, int(100 * base)))
+def test_oracle_reproduces_every_reference_artifact():
+    """All 174 reference configurations (every base x pop x alignment of both sweeps), two
+    seeds each, 100,000 yields (total_steps = 100000, grid_chain_sec11.py:342 -> 99,999 steps
+    after S0): wait.txt means per (graph, base, pop) and per (graph, base), and the final
+    |cut| / |B| distributions per base against the decoded end2 states (tests/reference_pin.py).
+    The device repeats this with eight seeds per configuration (test_reference_pin_gpu.py)."""
+    import reference_pin as RP
+    cfgs = RP.configs()
+    assert len(cfgs) == 174
+    jobs = [(c, s) for c in cfgs for s in (2001, 2002)]
     with ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
-        res = list(ex.map(_one_run, jobs))
-    ours = {}
-    for g, (w, cut) in zip(groups, res):
-        ours.setdefault(g, []).append(w)
-    for (tag, b), ws in ours.items():
-        keys = gold[f"{tag}_keys"]
-        ref = np.array([w for k, w in zip(keys, gold[f"{tag}_wait"]) if _parse(str(k))[1] == b], dtype=float)
-        assert ref.size in (12, 15)
-        diff = abs(np.mean(ws) - ref.mean())
-        tol = 4.0 * ref.std() * np.sqrt(1 / len(ws) + 1 / ref.size) + 1e-3 * ref.mean()
-        assert diff <= tol, (tag, b, np.mean(ws), ref.mean(), tol)
+        res = list(ex.map(_pin_run, jobs, chunksize=1))
+    worst = RP.check([(c, w, cut, nb) for (c, _), (w, cut, nb) in zip(jobs, res)])
+    assert worst["max_abs_z"] < RP.Z_MAX and worst["min_ks_p"] > RP.KS_P_MIN

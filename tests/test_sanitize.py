@@ -128,7 +128,7 @@ def _malformed():
     cases["degree_above_16"] = (21, star_row, star_col, np.ones(21, np.int32), star_pos, "degree")
     # positions that break the planar ring builder's assumptions: NaN, coincident, crossing
     p = pos.copy(); p[5] = [np.nan, 1.0]
-    cases["nan_position"] = (n, row, col, pop, p, None)
+    cases["nan_position"] = (n, row, col, pop, p, "finite")
     p = pos.copy(); p[6] = p[5]
     cases["coincident_positions"] = (n, row, col, pop, p, None)
     p = pos.copy(); p[[5, 10]] = p[[10, 5]]
