@@ -46,6 +46,8 @@ struct fc_run {
     int64_t *d_edge_acc = nullptr;
     int64_t *d_num_flips = nullptr, *d_part_sum = nullptr, *d_last_flipped = nullptr;
     int32_t *d_popk = nullptr;
+    int32_t *d_mcnt = nullptr, *d_ngk = nullptr;  // k > 2 district-graph rule tables
+    bool dgraph = false;
     int32_t wmax = 1;
     fc_event *d_events = nullptr;
     int64_t ev_cap = 0;
@@ -98,7 +100,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_events, r->d_prof, r->d_eta, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -296,6 +298,13 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     else         // fc_kernels.hip: a, fcnt, thresholds, BFS bitmaps, slots, district populations, wait queue
         r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + fc::bfs_bytes(n) + 5 * 64 * 4 + fc::kMaxKGeneral * 4 +
                              fc::kWaitQK * 16;
+    // k > 2: with every node's ring exact (all bounded faces triangles / quadrilaterals, so the
+    // rings list every face-adjacent cell) contiguity is decided by the district-graph rule
+    // (fc_kernels.hip district_rule) instead of the device search; FC_FLAG_FORCE_BFS keeps the
+    // search (cross-check)
+    r->dgraph = !recom && k > 2 && k <= fc::kMaxKDistrictRule && g.n_exact == n && g.planar && g.outer_simple &&
+                !(p->flags & FC_FLAG_FORCE_BFS);
+    if (r->dgraph) r->chain_lds_bytes += fc::dgraph_lds_bytes(k);
     r->wmax = 1;
     if (k > 2) r->wmax = p->wmax > 0 ? p->wmax : std::max(1, std::min(g.max_degree, k - 1));
 #ifdef FC_PHASE_PROF
@@ -348,6 +357,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     std::vector<uint8_t> fcnt((size_t)n_chains * r->npad, 0);
     std::vector<fc::ChainScalars> sc(n_chains);
     std::vector<int32_t> popk((size_t)n_chains * fc::kMaxKGeneral, 0);
+    std::vector<int32_t> mcnt(r->dgraph ? (size_t)n_chains * k * k : 0, 0), ngk(r->dgraph ? (size_t)n_chains * 32 : 0, 0);
     std::vector<uint64_t> thresh((size_t)n_chains * (2 * R + 1));
     std::vector<int32_t> q;
     std::vector<uint8_t> seen(n);
@@ -393,6 +403,20 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         s.pops[0] = (int32_t)pops[0];
         s.pops[1] = (int32_t)pops[1];
         for (int d = 0; d < fc::kMaxKGeneral; ++d) popk[(size_t)c * fc::kMaxKGeneral + d] = (int32_t)pops[d];
+        if (r->dgraph) {
+            // face-adjacent cell pairs {u, w} (w in ring(u), counted once: u < w) per district pair
+            int32_t *mc = &mcnt[(size_t)c * k * k];
+            for (int32_t u = 0; u < n; ++u) {
+                const int32_t L = (int32_t)(g.meta[u] & fc::kMetaLenMask);
+                for (int32_t j = 0; j < L; ++j) {
+                    const int32_t w = g.ring[(size_t)u * R + j];
+                    if (w <= u || a[w] == a[u]) continue;
+                    const int32_t X = std::min(a[u], a[w]), Y = std::max(a[u], a[w]);
+                    ++mc[X * k + Y];
+                }
+            }
+            for (int d = 0; d < k; ++d) ngk[(size_t)c * 32 + d] = ng[d];
+        }
         s.ngamma[0] = ng[0];
         s.ngamma[1] = ng[1];
         s.last_flip = -1;
@@ -463,6 +487,12 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     HIP_TRY(hipMemcpy(r->d_fcnt, fcnt.data(), fcnt.size(), hipMemcpyHostToDevice));
     if ((rc = dalloc(&r->d_popk, popk.size()))) return rc;
     HIP_TRY(hipMemcpy(r->d_popk, popk.data(), popk.size() * 4, hipMemcpyHostToDevice));
+    if (r->dgraph) {
+        if ((rc = dalloc(&r->d_mcnt, mcnt.size()))) return rc;
+        HIP_TRY(hipMemcpy(r->d_mcnt, mcnt.data(), mcnt.size() * 4, hipMemcpyHostToDevice));
+        if ((rc = dalloc(&r->d_ngk, ngk.size()))) return rc;
+        HIP_TRY(hipMemcpy(r->d_ngk, ngk.data(), ngk.size() * 4, hipMemcpyHostToDevice));
+    }
     if ((rc = dalloc(&r->d_sc, sc.size()))) return rc;
     HIP_TRY(hipMemcpy(r->d_sc, sc.data(), sc.size() * sizeof(sc[0]), hipMemcpyHostToDevice));
     if ((rc = dalloc(&r->d_thresh, thresh.size()))) return rc;
@@ -573,6 +603,9 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.n_chains = r->n_chains;
     k.k = r->p.k;
     k.popk = r->d_popk;
+    k.dgraph = r->dgraph ? 1 : 0;
+    k.mcnt = r->d_mcnt;
+    k.ngk = r->d_ngk;
     k.wmax = r->wmax;
     k.wthresh = (uint32_t)((1ull << 32) % (uint64_t)r->wmax);
     k.chain_lds_bytes = r->chain_lds_bytes;

@@ -19,6 +19,9 @@ inline int bfs_bytes(int n) { return 4 * bfs_lab_words(n) + 128 + 16 + 2 * 2 * 5
 inline int waves_per_block(int chain_lds_bytes) { return chain_lds_bytes > kBigChainLds ? 1 : kWavesPerBlock; }
 constexpr int kMaxK = 2;            // districts held in ChainScalars (k = 2 fast path)
 constexpr int kMaxKGeneral = 32;    // districts of the general (PAIR) kernel
+constexpr int kMaxKDistrictRule = 31;  // district-graph rule: bit 31 of a district mask is the outer face
+// LDS bytes of the district-graph rule's per-chain tables: pair counts, adjacency masks, outer counts
+inline int dgraph_lds_bytes(int k) { return 4 * k * k + 4 * 32 + 4 * 32; }
 
 // meta word layout (also exported by fc_graph_rings)
 constexpr uint64_t kMetaLenMask = 0xffull;
@@ -129,6 +132,12 @@ struct KParams {
     float prio_th[3];           // ... projected-finish / previous launch thresholds for priority 1/2/3
     int32_t wait_q;             // deferred-wait queue capacity in use (<= kWaitQ / kWaitQK)
     int32_t wpb;                // chains (waves) per workgroup: 1, 2 or 4
+    // k > 2 district-graph contiguity rule (every node exact, planar, simple outer face,
+    // k <= kMaxKDistrictRule): per chain, face-adjacent cell pairs per district pair and
+    // outer-face nodes per district (fc_kernels.hip district_rule)
+    int32_t dgraph;
+    int32_t *mcnt;              // [n_chains * k * k] pair counts, cell [min(X, Y) * k + max(X, Y)]
+    int32_t *ngk;               // [n_chains * 32] outer-face nodes per district
 };
 
 // Diagnostic build (-DFC_PHASE_PROF): s_memtime cycles per kernel phase, per chain.

@@ -36,6 +36,79 @@ namespace fc {
 
 using namespace dev;
 
+// District-graph contiguity rule (k > 2; every node exact, so each ring lists every cell that
+// shares a face with its node and the outer face is one wedge of the outer nodes' rings).
+//
+// Removing v from its district A disconnects A (single_flip_contiguous [gc-0.2],
+// grid_chain_sec11.py:22,340) iff two "super-gaps" of v's ring -- the stretches between
+// consecutive A-runs that hold old neighbours, made of other districts' cells, irrelevant
+// A-corners and (outer nodes) the outer-face wedge -- are joined through the complement of
+// A: cells of districts != A under face adjacency, plus the outer face.  (=>: a complement
+// path from one super-gap to another, closed through v, is a curve that separates the A-runs
+// on its two sides; no A edge can cross it, since it runs through face interiors and the
+// outer face.  <=: the boundary cycle around a piece cut off by v passes through v, entering
+// and leaving through two super-gaps, and otherwise through the complement.)  Every district
+// is connected, so the complement's components are those of the district graph without A:
+// X - Y when some face holds cells of both (adj, kept incrementally from the per-chain pair
+// counts), X - outer face when X has an outer-face node (bit 31).  The verdict is a few
+// bitmask closures -- no search.  Exactness holds for any such graph; the oracle's BFS is
+// the reference (tests/test_district_rule.py checks the restatement, the GPU parity tests the
+// kernel, per proposal).
+template <int RMAX>
+__device__ __forceinline__ bool district_rule(const int (&adv)[RMAX], uint32_t inA, uint32_t nbr, uint32_t Ln,
+                                              bool gam, int A, const uint32_t *adj) {
+    // ring augmented with the outer wedge (position Ln) for outer nodes
+    const uint32_t Lp = Ln + (gam ? 1u : 0u);
+    const uint32_t fullp = (1u << Lp) - 1u;
+    inA &= (1u << Ln) - 1u;
+    const uint32_t rotA = ((inA << 1) | (inA >> (Lp - 1))) & fullp;
+    uint32_t st0 = inA & ~rotA;  // run starts
+    const uint32_t a2 = inA | (inA << Lp);
+    uint32_t relA = 0;           // A-runs holding an old neighbour
+    while (st0) {
+        const int s0 = __builtin_ctz(st0);
+        st0 &= st0 - 1u;
+        const int len = __builtin_ctz(~(a2 >> s0));
+        uint32_t run = ((1u << len) - 1u) << s0;
+        run = (run | (run >> Lp)) & fullp;
+        if (run & nbr) relA |= run;
+    }
+    const uint32_t gap = fullp & ~relA;
+    const uint32_t rotG = ((gap << 1) | (gap >> (Lp - 1))) & fullp;
+    uint32_t gst = gap & ~rotG;  // super-gap starts
+    const uint32_t g2 = gap | (gap << Lp);
+    const uint32_t notA = ~(1u << A);
+    uint32_t seen = 0;
+    while (gst) {
+        const int s0 = __builtin_ctz(gst);
+        gst &= gst - 1u;
+        const int len = __builtin_ctz(~(g2 >> s0));
+        uint32_t run = ((1u << len) - 1u) << s0;
+        run = (run | (run >> Lp)) & fullp & ~inA;
+        uint32_t D = 0;          // districts of the super-gap's cells (+ the outer face)
+        while (run) {
+            const int i = __builtin_ctz(run);
+            run &= run - 1u;
+            uint32_t di = 1u << 31;  // position Ln: the outer wedge
+#pragma unroll
+            for (int q = 0; q < RMAX; ++q) di = (q == i) ? (1u << adv[q]) : di;
+            D |= di;
+        }
+        if (D & seen) return false;
+        uint32_t comp = D, fr = D;  // closure in the district graph without A
+        while (fr) {
+            const int X = __builtin_ctz(fr);
+            fr &= fr - 1u;
+            const uint32_t nb = adj[X] & notA & ~comp;
+            if (nb & seen) return false;
+            comp |= nb;
+            fr |= nb;
+        }
+        seen |= comp;
+    }
+    return true;
+}
+
 // KM = 2: two districts (BI_SIGN, and PAIR with k = 2, which coincide); the outer-face
 // exact rule applies.  KM = 0: k <= 32 districts, PAIR proposals, populations in LDS.
 // RMAX = 8: at most 128 VGPRs, four waves per SIMD (C3's 8192 chains per GPU run in two
@@ -73,6 +146,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     // after the flip, yields so far); as in fc_flip2.hip, drained by wait_flush
     uint64_t *q_d = (uint64_t *)(popk + kMaxKGeneral);
     uint32_t *q_nb = (uint32_t *)(q_d + kWaitQK), *q_run = q_nb + kWaitQK;
+    // district-graph rule (p.dgraph): pair counts [k * k], adjacency masks [32] (entry 31: the
+    // outer face), outer-face nodes per district [32]
+    int32_t *mcnt = (int32_t *)(q_run + kWaitQK);
+    uint32_t *adj = (uint32_t *)(mcnt + p.k * p.k);
+    int32_t *ngk = (int32_t *)(adj + 32);
+    const bool dgraph = KM == 0 && p.dgraph != 0;
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
     // ---- load the chain into LDS -------------------------------------------------------
@@ -85,6 +164,21 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         }
         if (lane < 2 * RMAX + 1) T[lane] = p.thresh[(size_t)c * (2 * RMAX + 1) + lane];
         if (KM == 0 && lane < 32) popk[lane] = p.popk[(size_t)c * 32 + lane];
+        if (dgraph) {
+            const int kk = p.k * p.k;
+            for (int i = lane; i < kk; i += kWave) mcnt[i] = p.mcnt[(size_t)c * kk + i];
+            if (lane < 32) ngk[lane] = p.ngk[(size_t)c * 32 + lane];
+            wave_sync();
+            // adj[X] bit Y: some face holds cells of X and Y; bit 31: X touches the outer face
+            uint32_t m = 0;
+            if (lane < p.k) {
+                for (int Y = 0; Y < p.k; ++Y)
+                    if (Y != lane && mcnt[min(lane, Y) * p.k + max(lane, Y)] > 0) m |= 1u << Y;
+                if (ngk[lane] > 0) m |= 1u << 31;
+            }
+            const uint32_t om = (uint32_t)__ballot(lane < p.k && ngk[lane] > 0);
+            if (lane < 32) adj[lane] = lane == 31 ? om : m;
+        }
     }
     ChainScalars *scp = p.sc + c;
     uint64_t draw = scp->draw;
@@ -209,6 +303,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         uint32_t tmask;      // neighbours in the target district
         int tgt;             // target district
         bool slot_ok = true;
+        int adv[RMAX];       // districts of the ring cells (KM = 0)
         if constexpr (KM == 2) {
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) inA |= (uint32_t)(a[ring_entry<RMAX>(rec.ring, i)] == av) << i;
@@ -216,7 +311,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             tgt = 1 - av;                       // -1 * assignment, grid_chain_sec11.py:145
             tmask = nbr & ~inA;
         } else {
-            int adv[RMAX];
             uint32_t dm = 0;                    // foreign districts among the neighbours
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) {
@@ -258,7 +352,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         // old neighbours on both sides.  Anything else multi-run goes to the device BFS.
         bool s_cut = false;
         if constexpr (KM == 0) {
-            if (has && !s_lin && nA > 0 && !force_bfs && !gam && (rec.meta & kMetaExact) && (link & full) == full) {
+            if (dgraph) {
+                // every multi-run case decided locally (district_rule above)
+                s_cut = has && !s_lin && nA > 0 && !district_rule<RMAX>(adv, inA, nbr, Ln, gam, av, adj);
+            } else if (has && !s_lin && nA > 0 && !force_bfs && !gam && (rec.meta & kMetaExact) && (link & full) == full) {
                 uint32_t relA = 0;
                 {
                     const uint32_t rotA = ((inA << 1) | (inA >> (Ln - 1))) & full;
@@ -347,6 +444,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 okN = gam ? s_cyc : s_lin;
             } else if (KM == 0 && s_cut) {
                 okT = okN = false;
+            } else if (KM == 0 && dgraph) {
+                okT = okN = true;  // one run, or the district rule found the pieces joined
             } else {
                 known = s_lin;
                 okT = okN = s_lin;
@@ -414,6 +513,41 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             }
             uint64_t ent = __ballot(enter);
             const int dnb = __popcll(ent) - __popcll(__ballot(leave));
+            // district-graph tables: the pairs {vf, w} of vf's face-adjacent cells w move from
+            // (Af, a[w]) to (tf, a[w]); a count crossing 0 flips an adjacency bit (as does an
+            // outer-face node crossing between districts), which may change the verdict of a
+            // later slot: the batch then ends after this flip
+            bool adj_chg = false;
+            if (dgraph) {
+                const int Lf = rl32((int)Ln, f);
+                bool chg = false;
+                if (lane < Lf) {
+                    const int X = a[my_e];
+                    if (X != Af && atomicSub(&mcnt[min(Af, X) * p.k + max(Af, X)], 1) == 1) {
+                        atomicAnd(&adj[Af], ~(1u << X));
+                        atomicAnd(&adj[X], ~(1u << Af));
+                        chg = true;
+                    }
+                    if (X != tf && atomicAdd(&mcnt[min(tf, X) * p.k + max(tf, X)], 1) == 0) {
+                        atomicOr(&adj[tf], 1u << X);
+                        atomicOr(&adj[X], 1u << tf);
+                        chg = true;
+                    }
+                }
+                if (lane == 0 && gamf) {
+                    if (atomicSub(&ngk[Af], 1) == 1) {
+                        atomicAnd(&adj[Af], ~(1u << 31));
+                        atomicAnd(&adj[31], ~(1u << Af));
+                        chg = true;
+                    }
+                    if (atomicAdd(&ngk[tf], 1) == 0) {
+                        atomicOr(&adj[tf], 1u << 31);
+                        atomicOr(&adj[31], 1u << tf);
+                        chg = true;
+                    }
+                }
+                adj_chg = __any(chg);
+            }
             if (lane == 0) {
                 a[vf] = (int8_t)tf;
                 fcnt[vf] = (uint8_t)(__popc(nbrf) - __popc(tmf));
@@ -442,6 +576,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             for (int i = 0; i < RMAX; ++i) hit |= v == (int)((rw[i >> 1] >> (16 * (i & 1))) & 0xffffu);
             const uint64_t aff = __ballot(hit && lane > f && lane < end);
             if (aff) end = __builtin_ctzll(aff);
+            if (adj_chg && f + 1 < end) end = f + 1;
             // non-hit draws after f whose node just entered the boundary would now propose
             if (ent) {
                 const int off_f = rl32(off_l, f);
@@ -651,6 +786,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             gf[i] = ((const uint4 *)fcnt)[i];
         }
         if (KM == 0 && lane < 32) p.popk[(size_t)c * 32 + lane] = popk[lane];
+        if (dgraph) {
+            const int kk = p.k * p.k;
+            for (int i = lane; i < kk; i += kWave) p.mcnt[(size_t)c * kk + i] = mcnt[i];
+            if (lane < 32) p.ngk[(size_t)c * 32 + lane] = ngk[lane];
+        }
     }
     int64_t cnt_prop = n_prop, cnt_acc = n_acc, cnt_ic = n_ic, cnt_ip = n_ip;
 #pragma unroll

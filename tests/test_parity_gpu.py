@@ -42,11 +42,13 @@ def _run_gpu(spec, inits, bases, *, steps, chunks=1, seed=11, pct=0.1, flags=0, 
     return fg, run
 
 
-def _check_chain(cref, spec, run, c, init, base, *, steps, seed=11, pct=0.1, tape=None, diag=True):
+def _check_chain(cref, spec, run, c, init, base, *, steps, seed=11, pct=0.1, tape=None, diag=True,
+                 trace_cap=500000):
     (_, _), (lo, hi) = G.population_bounds(int(spec.pop.sum()), 2, pct)
     ref = cref.run(spec, init, base=base, pop_lo=lo, pop_hi=hi, seed=seed, chain_id=c, n_steps=steps,
-                   log1mp=G.log1mp_table(spec.n, 2), trace_cap=500000, want_hist=diag, want_edges=diag,
+                   log1mp=G.log1mp_table(spec.n, 2), trace_cap=trace_cap, want_hist=diag, want_edges=diag,
                    want_flips=diag, tape=tape)
+    assert len(ref["trace"]) < trace_cap
     st = run.stats()
     tr = run.trace(c)
     rt = ref["trace"]
@@ -123,11 +125,26 @@ def test_tape_replay_matches_philox(gpu, cref, sec11):
 
 
 def test_c1_grid10(gpu, cref):
-    """BASELINE config C1: 10x10 grid, plan x[0] >= 5, base 1, pop tolerance 0.1."""
+    """BASELINE config C1 at its configured length: 10x10 grid, plan x[0] >= 5, base 1
+    (lambda = 1), pop tolerance 0.1, one chain of 1e5 yields (99,999 steps after S0), plus the
+    same chain at bases mu and 1/mu.  Every proposal, every per-yield tally (histograms,
+    cut_times, num_flips / part_sum / last_flipped) and the final state are bit-exact."""
     spec = G.grid_graph(10, 10)
-    init = spec.assignment_array(G.threshold_plan(spec.nodes, 0, 5), [-1, 1])[None, :]
-    _, run = _run_gpu(spec, init, np.asarray([1.0]), steps=20000)
-    _check_chain(cref, spec, run, 0, init[0], 1.0, steps=20000)
+    a0 = spec.assignment_array(G.threshold_plan(spec.nodes, 0, 5), [-1, 1])
+    inits = np.stack([a0] * 3)
+    bases = np.asarray([1.0, G.SEC11_MU, 1 / G.SEC11_MU])
+    steps = 99999
+    _, run = _run_gpu(spec, inits, bases, steps=steps, chunks=3, trace_cap=1500000)
+    ct = run.cut_times()
+    nf, ps, lf = run.flips()
+    ch, nh = run.hist()
+    for c in range(3):
+        ref = _check_chain(cref, spec, run, c, inits[c], bases[c], steps=steps, trace_cap=1500000)
+        assert np.array_equal(ct[c], ref["cut_times"])
+        assert np.array_equal(nf[c], ref["num_flips"]) and np.array_equal(ps[c], ref["part_sum"])
+        assert np.array_equal(lf[c], ref["last_flipped"])
+        assert np.array_equal(ch[c], ref["cut_hist"]) and np.array_equal(nh[c], ref["nb_hist"])
+        assert int(ch[c].sum()) == steps + 1
 
 
 def test_invalid_initial_state_raises(gpu, sec11):

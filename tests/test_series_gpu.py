@@ -111,6 +111,44 @@ def test_c4_triangular_k8_series(gpu, cref):
         assert np.array_equal(sums[c], es) and np.array_equal(acf[c], ea)
 
 
+def test_c4_full_size_triangular_k8(gpu, cref):
+    """BASELINE config C4 at its own size: nx.triangular_lattice_graph(100, 198) (N = 10,100,
+    deg <= 6), k = 8 vertical strips, pop tolerance 0.1, base in {1/mu_tri, 1, mu_tri}
+    (SURVEY §8(d)), with the event log, a hitting-time window and the device ACF on -- the
+    one-wave large-LDS layout of the k > 2 kernel at N ~ 10^4.  Per-proposal trace, events,
+    hitting time, lag sums and ACF against the oracle."""
+    spec = G.triangular_graph(100, 198)
+    assert spec.n == 10100
+    k = 8
+    plan = G.strip_plan(spec, k)
+    x0 = G.cut_and_boundary(spec, spec.assignment_array(plan, list(range(k))))[0]
+    mu_tri = 4.150797226
+    bases = [1 / mu_tri, 1.0, mu_tri, 1 / mu_tri, 1.0, mu_tri]
+    hit = (0, x0 - 6)
+    steps = 1200
+    run, inits = _setup(spec, k, plan, bases, pct=0.1, hit=hit, event_cap=steps + 1)
+    run.steps(200)
+    run.steps(steps - 200)
+    st = run.stats()
+    lags = [1, 2, 5, 17, 100, 640]
+    sums, acf = run.autocorr(lags)
+    assert int(st["bfs_calls"].sum()) > 0  # the large-graph search path is exercised
+    for c, b in enumerate(bases):
+        tr = _oracle_trace(cref, spec, k, inits[c], b, c, steps, 0.1)
+        got_tr = run.trace(c)
+        assert len(got_tr) == len(tr)
+        for f in ("draw", "v", "flags", "cut", "nb", "wait"):
+            assert np.array_equal(got_tr[f], tr[f]), (c, f)
+        x = yield_series(tr, x0)
+        got = run.events(c)
+        assert np.array_equal(np.stack([got["t"], got["v"], got["cut"], got["nb"], got["target"]], 1).astype(np.int64),
+                              events_from_trace(tr))
+        assert st["hit_time"][c] == hitting_time(x, *hit)
+        es, ea = acf_exact(x, lags)
+        assert np.array_equal(sums[c], es) and np.array_equal(acf[c], ea)
+        np.testing.assert_allclose(acf[c], acf_float(x, lags), rtol=0, atol=1e-9)
+
+
 def test_event_overflow_is_reported(gpu, sec11):
     run, _ = _setup(sec11, 2, G.sec11_plan(0, sec11.nodes), [1.0], pct=0.1, hit=(1, 0), event_cap=100)
     run.steps(3000)

@@ -11,7 +11,7 @@ from flipcomplexityempirical_amd import graphs as G
 from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune
 
 W = bench.Workload(sys.argv[1])
-C = int(sys.argv[2]) if len(sys.argv) > 2 else W.chains
+C = (int(sys.argv[2]) if len(sys.argv) > 2 else 0) or W.chains
 S = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
 IT = int(sys.argv[4]) if len(sys.argv) > 4 else 2
 fg = FlipGraph(W.spec)
