@@ -295,16 +295,16 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     else if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, 3 BFS bitmaps, slots, commit marks (2 npad + 16),
                       // wait queue (16 B per entry)
         r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16 + fc::kWaitQ * 16;
-    else         // fc_kernels.hip: a, fcnt, thresholds, BFS bitmaps, slots, district populations, wait queue
-        r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + fc::bfs_bytes(n) + 5 * 64 * 4 + fc::kMaxKGeneral * 4 +
-                             fc::kWaitQK * 16;
     // k > 2: with every node's ring exact (all bounded faces triangles / quadrilaterals, so the
     // rings list every face-adjacent cell) contiguity is decided by the district-graph rule
-    // (fc_kernels.hip district_rule) instead of the device search; FC_FLAG_FORCE_BFS keeps the
-    // search (cross-check)
+    // (fc_kernels.hip district_rule) instead of the device search, whose scratch is then not
+    // allocated; FC_FLAG_FORCE_BFS keeps the search (cross-check)
     r->dgraph = !recom && k > 2 && k <= fc::kMaxKDistrictRule && g.n_exact == n && g.planar && g.outer_simple &&
                 !(p->flags & FC_FLAG_FORCE_BFS);
-    if (r->dgraph) r->chain_lds_bytes += fc::dgraph_lds_bytes(k);
+    if (!recom && k > 2)  // fc_kernels.hip: a, fcnt, thresholds, [BFS scratch | district tables], slots,
+                          // district populations, wait queue
+        r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + (r->dgraph ? fc::dgraph_lds_bytes(k) : fc::bfs_bytes(n)) +
+                             5 * 64 * 4 + fc::kMaxKGeneral * 4 + fc::kWaitQK * 16;
     r->wmax = 1;
     if (k > 2) r->wmax = p->wmax > 0 ? p->wmax : std::max(1, std::min(g.max_degree, k - 1));
 #ifdef FC_PHASE_PROF
@@ -322,11 +322,14 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     // re-evaluation, 4 / 12 9.33, 4 / 20..64 8.9-9.0, 2 / 32 10.3, 8 / 32..64 9.45-9.55
     {
         auto &t = r->tune;
-        t.nsub = p->tune_nsub ? p->tune_nsub : (k == 2 ? 4 : 1);
-        if (!recom && !(k == 2 ? (t.nsub == 1 || t.nsub == 2 || t.nsub == 4) : (t.nsub == 1 || t.nsub == 2)))
-            return fail(FC_ERR_ARG, std::string("fc_run_create: tune_nsub must be ") +
-                                        (k == 2 ? "1, 2 or 4 for the k = 2 kernel" : "1 or 2 for the k > 2 kernel") +
-                                        " (got " + std::to_string(t.nsub) + ")");
+        // k > 2 (one MI355X, 2000-step launches): C3 (wmax 3) 1.80 / 2.14 / 2.09e9 proposals/s with
+        // 1 / 2 / 4 rounds, C4 (wmax 6) 6.6 / 7.9 / 7.6e8, C5 (wmax 16, ~39 draws per
+        // proposal) 3.0 / 4.1 / 4.8e8
+        const int wmax_k = k > 2 ? (p->wmax > 0 ? p->wmax : std::max(1, std::min(g.max_degree, k - 1))) : 1;
+        t.nsub = p->tune_nsub ? p->tune_nsub : (k == 2 ? 4 : wmax_k > 8 ? 4 : 2);
+        if (!recom && !(t.nsub == 1 || t.nsub == 2 || t.nsub == 4))
+            return fail(FC_ERR_ARG, std::string("fc_run_create: tune_nsub must be 1, 2 or 4 for the ") +
+                                        (k == 2 ? "k = 2" : "k > 2") + " kernel (got " + std::to_string(t.nsub) + ")");
         t.hit_stop = p->tune_hit_stop ? p->tune_hit_stop : 32;
         if (t.hit_stop < 1) return fail(FC_ERR_ARG, "fc_run_create: tune_hit_stop must be >= 1");
         t.par_min = p->tune_par_min ? p->tune_par_min : 3;

@@ -140,7 +140,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     bs.nxt = bs.front + p.words;
     bs.W = p.words;
     bs.prof = nullptr;
-    uint32_t *slot = (uint32_t *)(bs.nxt + p.words);  // [5][64]: node, word1, word2, draw offset, word3
+    // [5][64]: node, word1, word2, draw offset, word3; with the district-graph rule the search
+    // never runs and its scratch is not allocated (fc_run_create)
+    uint32_t *slot = KM == 0 && p.dgraph ? (uint32_t *)(T + (2 * RMAX + 2)) : (uint32_t *)(bs.nxt + p.words);
     int32_t *popk = (int32_t *)(slot + 5 * 64);    // [32] district populations (KM = 0)
     // accepted states whose geometric wait is still to be drawn (kWaitQK: creating draw, |B|
     // after the flip, yields so far); as in fc_flip2.hip, drained by wait_flush
@@ -257,8 +259,19 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             }
             const uint64_t m = (uint64_t)w.x0 * (uint64_t)(uint32_t)n;
             const int v = (int)(m >> 32);
-            const bool ok = inrange && (uint32_t)m >= p.lemire_thresh;
-            const bool hit = ok && fcnt[v] != 0;
+            bool ok = inrange && (uint32_t)m >= p.lemire_thresh;
+            bool hit;
+            if constexpr (KM == 0) {
+                // the draw's district slot r (word 3, exact Lemire over wmax) can only name a
+                // foreign district if r < fcnt[v] (foreign neighbours >= foreign districts):
+                // slots beyond are non-proposals whatever 1b would find, so they take no slot
+                // (a slot rejected by the Lemire map never proposes: not a non-hit either)
+                const uint64_t mw = (uint64_t)w.x3 * (uint64_t)(uint32_t)p.wmax;
+                ok = ok && (uint32_t)mw >= p.wthresh;
+                hit = ok && (int)(mw >> 32) < (int)fcnt[v];
+            } else {
+                hit = ok && fcnt[v] != 0;
+            }
             const uint64_t hm = __ballot(hit);
             const int pos = nh + __popcll(hm & bits_below(lane));
             if (hit && pos < 64) {
@@ -511,8 +524,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 enter = dlt > 0 && old == 0;
                 leave = dlt < 0 && old == 1;
             }
-            uint64_t ent = __ballot(enter);
-            const int dnb = __popcll(ent) - __popcll(__ballot(leave));
+            // non-hit draws to re-check below: nodes that entered the boundary; with PAIR
+            // slots (KM = 0) any node whose foreign-neighbour count grew (its slot may now
+            // fall below it)
+            uint64_t ent = __ballot(KM == 0 ? (is_nbr && dlt > 0) : enter);
+            const int dnb = __popcll(__ballot(enter)) - __popcll(__ballot(leave));
             // district-graph tables: the pairs {vf, w} of vf's face-adjacent cells w move from
             // (Af, a[w]) to (tf, a[w]); a count crossing 0 flips an adjacency bit (as does an
             // outer-face node crossing between districts), which may change the verdict of a
@@ -863,6 +879,7 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, siz
     switch (p.nsub) {                                 \
         case 1: FC_FULL_SWITCH(R, 1, K); break;       \
         case 2: FC_FULL_SWITCH(R, 2, K); break;       \
+        case 4: FC_FULL_SWITCH(R, 4, K); break;       \
         default: return (int)hipErrorInvalidValue;    \
     }
     if (ring_max == 8) {

@@ -201,12 +201,13 @@ def test_k4_wait_queue_lengths(gpu, cref, sec11, wait_queue):
 
 def test_tuning_fields_checked(gpu, sec11):
     """Out-of-range launch tuning is an FC_ERR_ARG (ValueError) naming the field and the kernel,
-    never a generic HIP launch failure (FC_NSUB=4 used to break every k > 2 launch)."""
+    never a generic HIP launch failure (an out-of-range FC_NSUB used to break every k > 2
+    launch)."""
     fg = FlipGraph(sec11)
     a4 = sec11.assignment_array(G.quadrant_plan(sec11.nodes), list(range(4)))
     _, (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 4, 0.05)
     base = RunConfig(k=4, labels=tuple(range(4)), proposal=_lib.FC_PROPOSE_PAIR, seed=1, pop_lo=lo, pop_hi=hi)
-    for bad, what in (({"nsub": 4}, "k > 2"), ({"wait_queue": 33}, "tune_wait_queue"),
+    for bad, what in (({"nsub": 3}, "k > 2"), ({"wait_queue": 33}, "tune_wait_queue"),
                       ({"chains_per_block": 3}, "tune_chains_per_block")):
         cfg = RunConfig(**{**base.__dict__, "tune": bad})
         with pytest.raises(ValueError, match=what):

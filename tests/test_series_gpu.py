@@ -21,7 +21,7 @@ DIAG = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_SERIES
 LAGS = [1, 2, 3, 7, 16, 100, 1000, 4097, 5000]
 
 
-def _setup(spec, k, plan, bases, *, pct, hit, event_cap=200000, proposal=None, seed=31):
+def _setup(spec, k, plan, bases, *, pct, hit, event_cap=200000, proposal=None, seed=31, flags=0):
     fg = FlipGraph(spec)
     _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
     labels = [-1, 1] if k == 2 else list(range(k))
@@ -30,7 +30,7 @@ def _setup(spec, k, plan, bases, *, pct, hit, event_cap=200000, proposal=None, s
     cfg = RunConfig(k=k, labels=tuple(labels) if k == 2 else tuple(range(k)),
                     proposal=(_lib.FC_PROPOSE_BI_SIGN if k == 2 else _lib.FC_PROPOSE_PAIR) if proposal is None else proposal,
                     seed=seed, pop_lo=lo, pop_hi=hi, diag_mask=DIAG, trace_chains=len(bases), trace_cap=400000,
-                    hit_lo=hit[0], hit_hi=hit[1], event_cap=event_cap)
+                    hit_lo=hit[0], hit_hi=hit[1], event_cap=event_cap, flags=flags)
     return FlipRun(fg, inits, cfg, bases=np.asarray(bases)), inits
 
 
@@ -111,12 +111,14 @@ def test_c4_triangular_k8_series(gpu, cref):
         assert np.array_equal(sums[c], es) and np.array_equal(acf[c], ea)
 
 
-def test_c4_full_size_triangular_k8(gpu, cref):
+@pytest.mark.parametrize("force_bfs", [False, True])
+def test_c4_full_size_triangular_k8(gpu, cref, force_bfs):
     """BASELINE config C4 at its own size: nx.triangular_lattice_graph(100, 198) (N = 10,100,
     deg <= 6), k = 8 vertical strips, pop tolerance 0.1, base in {1/mu_tri, 1, mu_tri}
     (SURVEY §8(d)), with the event log, a hitting-time window and the device ACF on -- the
-    one-wave large-LDS layout of the k > 2 kernel at N ~ 10^4.  Per-proposal trace, events,
-    hitting time, lag sums and ACF against the oracle."""
+    one-wave large-LDS layout of the k > 2 kernel at N ~ 10^4, with contiguity decided by the
+    district-graph rule (no search) and, forced, by the device search.  Per-proposal trace,
+    events, hitting time, lag sums and ACF against the oracle."""
     spec = G.triangular_graph(100, 198)
     assert spec.n == 10100
     k = 8
@@ -126,13 +128,17 @@ def test_c4_full_size_triangular_k8(gpu, cref):
     bases = [1 / mu_tri, 1.0, mu_tri, 1 / mu_tri, 1.0, mu_tri]
     hit = (0, x0 - 6)
     steps = 1200
-    run, inits = _setup(spec, k, plan, bases, pct=0.1, hit=hit, event_cap=steps + 1)
+    run, inits = _setup(spec, k, plan, bases, pct=0.1, hit=hit, event_cap=steps + 1,
+                        flags=_lib.FC_FLAG_FORCE_BFS if force_bfs else 0)
     run.steps(200)
     run.steps(steps - 200)
     st = run.stats()
     lags = [1, 2, 5, 17, 100, 640]
     sums, acf = run.autocorr(lags)
-    assert int(st["bfs_calls"].sum()) > 0  # the large-graph search path is exercised
+    if force_bfs:
+        assert int(st["bfs_calls"].sum()) > 0  # the large-graph search path is exercised
+    else:
+        assert int(st["bfs_calls"].sum()) == 0  # every multi-run case decided by the district rule
     for c, b in enumerate(bases):
         tr = _oracle_trace(cref, spec, k, inits[c], b, c, steps, 0.1)
         got_tr = run.trace(c)
