@@ -85,10 +85,10 @@ class Workload:
             self.bases = [1 / MU_TRI, 1.0, MU_TRI]
             self._plans = [self.spec.assignment_array(G.strip_plan(self.spec, 8), self.labels)]
             self.plan_of = lambda g: 0
-            self.chains = 2048
+            self.chains = 2048  # bench sizes it to the resident capacity (resident_chains)
             self.R, self.W = r_bytes(6, 0), w_bytes(6)
             self.desc = (f"C4: triangular lattice 100x198 (N={self.spec.n}), k=8 vertical strips, pair proposals, "
-                         "pop tol 0.1, base in {1/mu_tri, 1, mu_tri}, 2048 chains/GPU")
+                         "pop tol 0.1, base in {1/mu_tri, 1, mu_tri}, one wave of resident chains per GPU")
         elif name == "c5":
             self.spec = G.delaunay_graph(10000, seed=0)
             self.k, self.pct, self.proposal = 18, 0.1, _lib.FC_PROPOSE_PAIR
@@ -100,7 +100,8 @@ class Workload:
             d = float(self.spec.degree().mean())
             self.R, self.W = r_bytes(d, 0), w_bytes(d)
             self.desc = ("C5: Delaunay dual of 10^4 uniform points (E=%d), lognormal pops, k=18 bisection plan, "
-                         "pair proposals, pop tol 0.1, base in {0.5, 1, 2}, 2048 chains/GPU" % self.spec.n_edges)
+                         "pair proposals, pop tol 0.1, base in {0.5, 1, 2}, one wave of resident chains per GPU"
+                         % self.spec.n_edges)
         else:
             raise ValueError(f"unknown workload {name}")
         self.seed = SEED + {"c2": 0, "c3": 1, "c4": 2, "c5": 3}[name]
@@ -110,6 +111,20 @@ class Workload:
 
     def init_of(self, g):
         return self._plans[self.plan_of(g)]
+
+
+def resident_chains(fg, W, device: int = 0) -> int:
+    """Chains one GPU holds at once for workload W: CUs x min(LDS / chain LDS, 16 waves)."""
+    import torch
+    from flipcomplexityempirical_amd import graphs as G
+    from flipcomplexityempirical_amd.engine import FlipRun, RunConfig
+    _, (lo, hi) = G.population_bounds(int(W.spec.pop.sum()), W.k, W.pct)
+    probe = FlipRun(fg, W.init_of(0)[None, :], RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal,
+                                                         pop_lo=lo, pop_hi=hi, device=device))
+    lds = probe.chain_lds_bytes()
+    probe.close()
+    cus = torch.cuda.get_device_properties(device).multi_processor_count if torch.cuda.is_available() else 256
+    return cus * max(1, min(160 * 1024 // lds, 16))
 
 
 def _dist():
@@ -247,6 +262,10 @@ def main():
     fg = FlipGraph(spec)
     from flipcomplexityempirical_amd import distributed as D
     C = args.chains or W.chains
+    if not args.chains and W.name in ("c4", "c5"):
+        # large graphs: one chain per workgroup, LDS-bound residency; size the launch to one
+        # wave of resident chains (a second, partial wave would double the launch time)
+        C = resident_chains(fg, W, local_rank)
     off, cnt = D.shard(C * world, world, rank)          # weak scaling: C chains per GPU
     gids = np.arange(off, off + cnt)
     inits = np.stack([W.init_of(int(g)) for g in gids])

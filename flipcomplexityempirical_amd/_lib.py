@@ -32,7 +32,7 @@ EXPORTED = [
     "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_read_recom_trace",
     "fc_run_trace_reset", "fc_run_read_hist",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
-    "fc_run_frame_series", "fc_run_kernel_name", "fc_run_n_chains", "fc_run_destroy",
+    "fc_run_frame_series", "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
 ]
 
@@ -146,13 +146,16 @@ def load(build_if_missing: bool = True):
     L.fc_run_kernel_name.argtypes = [vp, ctypes.c_char_p, i32]
     L.fc_run_n_chains.argtypes = [vp]
     L.fc_run_n_chains.restype = i32
+    L.fc_run_chain_lds_bytes.argtypes = [vp]
+    L.fc_run_chain_lds_bytes.restype = i32
     L.fc_run_destroy.argtypes = [vp]
     L.fc_run_destroy.restype = None
     L.fc_device_count.argtypes = [_P(i32)]
     L.fc_last_error.argtypes = []
     L.fc_last_error.restype = ctypes.c_char_p
     for name in EXPORTED:
-        if name not in ("fc_graph_destroy", "fc_run_destroy", "fc_last_error", "fc_run_n_chains"):
+        if name not in ("fc_graph_destroy", "fc_run_destroy", "fc_last_error", "fc_run_n_chains",
+                        "fc_run_chain_lds_bytes"):
             getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

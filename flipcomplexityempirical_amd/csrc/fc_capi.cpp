@@ -217,6 +217,8 @@ void fc_graph_destroy(fc_graph *g) { delete g; }
 
 int32_t fc_run_n_chains(const fc_run *r) { return r ? r->n_chains : 0; }
 
+int32_t fc_run_chain_lds_bytes(const fc_run *r) { return r ? r->chain_lds_bytes : 0; }
+
 int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, const int8_t *init_assign,
                   const double *bases, fc_run **out) {
     if (!out) return fail(FC_ERR_ARG, "fc_run_create: null output");

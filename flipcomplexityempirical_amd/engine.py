@@ -378,6 +378,10 @@ class FlipRun:
         bounds = np.concatenate([[t0], ev["t"], [T + 1]]).astype(np.int64)
         return np.repeat(np.asarray(values)[:ev.size + 1], np.diff(bounds))
 
+    def chain_lds_bytes(self) -> int:
+        """LDS bytes of one chain's device state (``fc_run_chain_lds_bytes``)."""
+        return int(_lib.load().fc_run_chain_lds_bytes(self.handle))
+
     def kernel_name(self) -> str:
         """The flip-kernel instance the last ``steps`` call launched (rocprofv3 spelling)."""
         buf = ctypes.create_string_buffer(128)

@@ -286,6 +286,10 @@ int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, cons
 /* Name of the last launched flip-kernel instance, as rocprofv3 spells it. */
 int fc_run_kernel_name(const fc_run *r, char *buf, int32_t cap);
 int32_t fc_run_n_chains(const fc_run *r);
+/* LDS bytes one chain's state takes on the device (one chain per wavefront; the chains a CU
+ * holds at once is 160 KiB / this, or the VGPR limit) -- for sizing launches to one wave of
+ * resident chains. */
+int32_t fc_run_chain_lds_bytes(const fc_run *r);
 void fc_run_destroy(fc_run *r);
 
 int fc_device_count(int32_t *n);

@@ -11,10 +11,11 @@ from flipcomplexityempirical_amd import graphs as G
 from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune
 
 W = bench.Workload(sys.argv[1])
-C = (int(sys.argv[2]) if len(sys.argv) > 2 else 0) or W.chains
 S = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
 IT = int(sys.argv[4]) if len(sys.argv) > 4 else 2
 fg = FlipGraph(W.spec)
+C = (int(sys.argv[2]) if len(sys.argv) > 2 else 0) or (bench.resident_chains(fg, W) if W.name in ("c4", "c5")
+                                                         else W.chains)
 inits = np.stack([W.init_of(g) for g in range(C)])
 bases = np.asarray([W.base_of(g) for g in range(C)])
 _, (lo, hi) = G.population_bounds(int(W.spec.pop.sum()), W.k, W.pct)
