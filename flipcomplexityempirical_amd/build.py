@@ -15,7 +15,7 @@ CSRC = os.path.join(PKG, "csrc")
 # (prof: per-phase s_memtime counters; sync: each stamp drains outstanding memory first).
 VARIANT = os.environ.get("FC_LIB_VARIANT", "")
 VARIANT_FLAGS = {"prof": "-DFC_PHASE_PROF", "sync": "-DFC_PHASE_SYNC"}
-LIB = os.path.join(PKG, f"libflipchain_{VARIANT}.so" if VARIANT else "libflipchain.so")
+LIB = os.environ.get("FC_LIB_OUT") or os.path.join(PKG, f"libflipchain_{VARIANT}.so" if VARIANT else "libflipchain.so")
 SOURCES = ["fc_flip2.hip", "fc_kernels.hip", "fc_series.hip", "fc_recom.hip", "fc_capi.cpp", "fc_graph.cpp"]
 HEADERS = ["fc_internal.h", "fc_philox.h", "fc_device.h", os.path.join("..", "..", "include", "flipchain.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -37,6 +37,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
            "-Wall", "-Wno-unused-function", "-o", LIB]
     for tok in filter(None, VARIANT.split("_")):
         cmd.insert(-2, VARIANT_FLAGS[tok])
+    # FC_HIPCC_FLAGS: extra compiler flags for experiment builds (with FC_LIB_OUT naming the output)
+    cmd[-2:-2] = os.environ.get("FC_HIPCC_FLAGS", "").split()
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), flush=True)

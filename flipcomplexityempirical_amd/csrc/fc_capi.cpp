@@ -63,7 +63,7 @@ struct fc_run {
     char kname[96] = {0};        // last launched flip-kernel instance
     bool variant = false;        // accept / constraint variants (FULL k = 2 instance)
     struct {                     // fc_params.tune_* with the defaults filled in
-        int32_t nsub, hit_stop, par_min, wait_q, wpb;
+        int32_t nsub, hit_stop, par_min, wait_q, wpb, coop;
         int32_t prio_div[3];     // prio_div[0] <= 0: priorities off
         float prio_th[3];
     } tune{};
@@ -344,6 +344,16 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         if (t.wpb != 1 && t.wpb != 2 && t.wpb != 4)
             return fail(FC_ERR_ARG, "fc_run_create: tune_chains_per_block must be 1, 2 or 4");
         t.wpb = std::min(t.wpb, fc::waves_per_block(r->chain_lds_bytes));
+        // large k > 2 chains that need the search: 4 = one chain per 256-thread workgroup,
+        // searched by all of it.  Default 1: the workgroup's helper waves carry the kernel's
+        // VGPR count, so a chain then holds four waves' registers and fewer chains are
+        // resident, and these searches are short (≈ 2 levels from the C4 / C5 start plans):
+        // C4 forced search 5.7 ms (1 wave) against 7.3 ms (workgroup), C5 7.9 against 16.8,
+        // C5 without positions 11.7 against 28.1 (1024 chains x 1000 steps, one MI355X)
+        const int sw = p->tune_search_waves ? p->tune_search_waves : 1;
+        if (sw != 1 && sw != 4) return fail(FC_ERR_ARG, "fc_run_create: tune_search_waves must be 1 or 4");
+        t.coop = !recom && k > 2 && !r->dgraph && r->chain_lds_bytes > fc::kBigChainLds && sw == 4;
+        if (t.coop) r->chain_lds_bytes += 32 * 4;  // control words of the cooperative search
         // k = 2: chains with a short boundary need many draws per proposal and set the launch
         // time; they get the SIMD's issue priority over the chains sharing it (s_setprio 1/2/3
         // below |B| = n/2, n/5, n/10); once a chain has taken 1/16 of its steps, its projected
@@ -653,6 +663,7 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.par_min = r->tune.par_min;
     k.wait_q = r->tune.wait_q;
     k.wpb = r->tune.wpb;
+    k.coop = r->tune.coop ? 1 : 0;
     k.variant = r->variant ? 1 : 0;
     k.accept = r->p.accept;
     k.con_valid = r->p.con_valid;

@@ -302,6 +302,189 @@ __device__ __forceinline__ bool wave_bfs(const NodeRec<RMAX> *__restrict__ G, co
     }
 }
 
+// Workgroup-cooperative form of the multi-source search, for large graphs whose chain has a
+// workgroup to itself (one chain per workgroup; SURVEY §5 "one workgroup per chain with a
+// cooperative LDS BFS").  Every thread of the workgroup expands frontier nodes; the chain's
+// wave issues the search and the other waves wait for it at a barrier (coop_helper_loop).
+//
+// A node's label byte (label + 1; 0 = unvisited, 0xff = the removed node v) is claimed with
+// one LDS compare-and-swap on its dword, so the claim and the label are one atomic step and a
+// losing thread reads the winner's label from the swap's result, whatever wave won.  Appends
+// go to the next level's list through an LDS counter (overflow to a bitmap); merges and live
+// labels collect in LDS masks; after a barrier the chain's wave closes the component masks
+// and decides (connected / disconnected / go on), and a second barrier publishes it.
+// Control words (ctl, 32 ints): 0 cmd, 1 vf, 2 A, 3 ns, 4 decision, 5 live, 6 merged,
+// 7 spill_out, 8 spill_in, 9-10 list lengths, 16-31 source nodes.
+enum : int { kCtlCmd = 0, kCtlVf, kCtlA, kCtlNs, kCtlDec, kCtlLive, kCtlMerged, kCtlSpillOut, kCtlSpillIn,
+             kCtlLen0, kCtlLen1, kCtlSrc = 16 };
+
+__device__ __forceinline__ void block_sync() { __syncthreads(); }
+
+template <int RMAX>
+__device__ bool coop_bfs(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, const BfsScratch &S,
+                         int32_t *ctl, int tid, int nthr, int64_t &levels) {
+    // every value that steers a barrier is made wave-uniform (readfirstlane), so the compiler
+    // never executes a barrier on a masked path
+    const int W = S.W;
+    const int vf = __builtin_amdgcn_readfirstlane(ctl[kCtlVf]), A = __builtin_amdgcn_readfirstlane(ctl[kCtlA]),
+              ns = __builtin_amdgcn_readfirstlane(ctl[kCtlNs]);
+    uint8_t *const lab = (uint8_t *)S.lab;
+    for (int i = tid; i < S.lab_words; i += nthr) S.lab[i] = 0;
+    for (int i = tid; i < W; i += nthr) {
+        S.front[i] = 0;
+        S.nxt[i] = 0;
+    }
+    if (tid < 16) {
+        S.mm[tid] = 0;
+        S.cm[tid] = 1u << tid;
+    }
+    block_sync();
+    if (tid < ns) {
+        const int x = ctl[kCtlSrc + tid];
+        lab[x] = (uint8_t)(tid + 1);
+        S.list[tid] = (uint16_t)x;
+    }
+    if (tid == 0) {
+        lab[vf] = 0xff;
+        ctl[kCtlLen0] = ns;
+        ctl[kCtlLen1] = 0;
+        ctl[kCtlLive] = 0;
+        ctl[kCtlMerged] = 0;
+        ctl[kCtlSpillOut] = 0;
+        ctl[kCtlSpillIn] = 0;
+    }
+    block_sync();
+    const uint32_t all = (uint32_t)((1ull << ns) - 1ull);
+    for (int cur = 0;; cur ^= 1) {
+        if (tid == 0) ++levels;
+        const int fcur = __builtin_amdgcn_readfirstlane(ctl[kCtlLen0 + cur]);
+        const bool spill_in = __builtin_amdgcn_readfirstlane(ctl[kCtlSpillIn]) != 0;
+        uint16_t *const lcur = S.list + cur * kBfsList, *const lnxt = S.list + (cur ^ 1) * kBfsList;
+        uint32_t live = 0;
+        bool merged = false, spill = false;
+        auto expand = [&](int u) {
+            const uint32_t la = (uint32_t)lab[u] - 1u;  // this node's label
+            const uint32_t cla = S.cm[la & 15u];
+            const NodeRec<RMAX> rr = G[u];
+            const uint32_t nbr = (uint32_t)(rr.meta >> kMetaNbrShift) & 0xffffu;
+            uint32_t hit = 0;
+#pragma unroll
+            for (int j = 0; j < RMAX; ++j) {
+                if (!((nbr >> j) & 1u)) continue;
+                const int w = ring_entry<RMAX>(rr.ring, j);
+                if (w == vf || a[w] != A) continue;
+                uint32_t *wd = S.lab + (w >> 2);
+                const int sh = 8 * (w & 3);
+                uint32_t old = *wd, other = 0;
+                for (;;) {
+                    other = (old >> sh) & 0xffu;
+                    if (other) break;
+                    const uint32_t prev = atomicCAS(wd, old, old | ((la + 1u) << sh));
+                    if (prev == old) break;
+                    old = prev;
+                }
+                if (!other) {  // won: w joins the next level
+                    live |= 1u << la;
+                    const int pos = atomicAdd(&ctl[kCtlLen0 + (cur ^ 1)], 1);
+                    if (pos < kBfsList) {
+                        lnxt[pos] = (uint16_t)w;
+                    } else {
+                        atomicOr((unsigned long long *)&S.nxt[w >> 6], 1ull << (w & 63));
+                        spill = true;
+                    }
+                } else if (other != 0xffu && !((cla >> (other - 1u)) & 1u)) {
+                    hit |= 1u << (other - 1u);  // ran into another component
+                }
+            }
+            if (hit) {
+                atomicOr(&S.mm[la], hit);
+                merged = true;
+            }
+        };
+        const int Fl = min(fcur, kBfsList);
+        for (int q = tid; q < Fl; q += nthr) expand((int)lcur[q]);
+        if (spill_in) {
+            for (int i = tid; i < W; i += nthr) {
+                uint64_t bits = S.front[i];
+                while (bits) {
+                    const int b = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    expand(i * 64 + b);
+                }
+            }
+        }
+        if (live) atomicOr((uint32_t *)&ctl[kCtlLive], live);
+        if (merged) atomicOr(&ctl[kCtlMerged], 1);
+        if (spill) atomicOr(&ctl[kCtlSpillOut], 1);
+        block_sync();
+        if (tid < kWave) {  // the first wave decides
+            const int lane = tid;
+            uint32_t comp = lane < 16 ? S.cm[lane] : 0u;
+            if (ctl[kCtlMerged]) {
+                const uint32_t adj = comp | (lane < 16 ? S.mm[lane] : 0u);
+                uint32_t sym = adj;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t aj = (uint32_t)__shfl((int)adj, j);
+                    if (lane < 16 && ((aj >> lane) & 1u)) sym |= 1u << j;
+                }
+                comp = lane < 16 ? sym : 0u;
+                for (int it = 0; it < 4; ++it) {
+                    uint32_t nx = comp;
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const uint32_t cj = (uint32_t)__shfl((int)comp, j);
+                        if ((comp >> j) & 1u) nx |= cj;
+                    }
+                    const bool ch = nx != comp;
+                    comp = nx;
+                    if (!__any(ch)) break;
+                }
+                if (lane < 16) {
+                    S.mm[lane] = 0;
+                    S.cm[lane] = comp;
+                }
+            }
+            const uint32_t lv = (uint32_t)ctl[kCtlLive];
+            int dec = 0;
+            if ((((uint32_t)__shfl((int)comp, 0)) & all) == all) dec = 1;                  // one component
+            else if (__any(lane < ns && (comp & lv) == 0u)) dec = 2;                        // a closed piece
+            wave_sync();
+            if (lane == 0) {
+                ctl[kCtlDec] = dec;
+                ctl[kCtlSpillIn] = ctl[kCtlSpillOut];
+                ctl[kCtlSpillOut] = 0;
+                ctl[kCtlLive] = 0;
+                ctl[kCtlMerged] = 0;
+                ctl[kCtlLen0 + cur] = 0;  // this level's list is refilled two levels on
+            }
+        }
+        block_sync();
+        const int dec = __builtin_amdgcn_readfirstlane(ctl[kCtlDec]);
+        if (dec) return dec == 1;
+        if (__builtin_amdgcn_readfirstlane(ctl[kCtlSpillIn])) {  // the next level expands the overflow bitmap too
+            for (int i = tid; i < W; i += nthr) {
+                S.front[i] = S.nxt[i];
+                S.nxt[i] = 0;
+            }
+            block_sync();
+        }
+    }
+}
+
+// The helper waves of a cooperative chain: wait for a search command, take part, repeat
+// until the chain's wave sends the exit command (ctl[kCtlCmd] = 0).
+template <int RMAX>
+__device__ void coop_helper_loop(const NodeRec<RMAX> *__restrict__ G, const int8_t *a, const BfsScratch &S,
+                                 int32_t *ctl, int tid, int nthr) {
+    int64_t dummy = 0;
+    for (;;) {
+        block_sync();
+        if (__builtin_amdgcn_readfirstlane(ctl[kCtlCmd]) == 0) return;
+        (void)coop_bfs<RMAX>(G, a, S, ctl, tid, nthr, dummy);
+    }
+}
+
 // Register-light single-source form for the k = 2 kernel, where the planar rule decides
 // every node of the reference's lattices and the search is the rare fallback: are all
 // old-district neighbours (lanes < RMAX hold them in my_target) reached from `start`?

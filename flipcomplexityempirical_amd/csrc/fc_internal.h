@@ -138,6 +138,8 @@ struct KParams {
     int32_t dgraph;
     int32_t *mcnt;              // [n_chains * k * k] pair counts, cell [min(X, Y) * k + max(X, Y)]
     int32_t *ngk;               // [n_chains * 32] outer-face nodes per district
+    int32_t coop;               // k > 2 large graphs without the district rule: one chain per
+                                // 256-thread workgroup, contiguity searches by the whole workgroup
 };
 
 // Diagnostic build (-DFC_PHASE_PROF): s_memtime cycles per kernel phase, per chain.

@@ -119,12 +119,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int c = (int)blockIdx.x * (int)(blockDim.x >> 6) + wv;
+    // p.coop: one chain per workgroup; wave 0 runs it, waves 1.. join its contiguity searches
+    const bool coop = KM == 0 && p.coop != 0;
+    const int c = coop ? (int)blockIdx.x : (int)blockIdx.x * (int)(blockDim.x >> 6) + wv;
     if (c >= p.n_chains) return;
 
     const int n = p.n;
     const int npad = (n + 15) & ~15;
-    unsigned char *base = smem + (size_t)wv * p.chain_lds_bytes;
+    unsigned char *base = smem + (coop ? (size_t)0 : (size_t)wv * p.chain_lds_bytes);
     int8_t *a = (int8_t *)base;
     uint8_t *fcnt = base + npad;
     uint64_t *T = (uint64_t *)(base + 2 * npad);
@@ -154,7 +156,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     uint32_t *adj = (uint32_t *)(mcnt + p.k * p.k);
     int32_t *ngk = (int32_t *)(adj + 32);
     const bool dgraph = KM == 0 && p.dgraph != 0;
+    // cooperative search control words (coop implies no district tables: they start here)
+    int32_t *ctl = (int32_t *)(q_run + kWaitQK);
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
+    if (coop && wv > 0) {
+        coop_helper_loop<RMAX>(G, a, bs, ctl, (int)threadIdx.x, (int)blockDim.x);
+        return;
+    }
 
     // ---- load the chain into LDS -------------------------------------------------------
     {
@@ -436,8 +444,29 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
             ++bfs_calls;
             FC_STAMP(t_b0);
-            const bool res = wave_bfs<RMAX>(G, a, bs, lane, (int)(pkf & 0x7fffu), (int)((pkf >> 15) & 63u), my_target,
-                                            bfs_levels);
+            bool res;
+            if (coop) {
+                // hand the search to the whole workgroup (coop_bfs): sources by label order
+                const bool srcl = my_target >= 0;
+                const uint64_t SM = __ballot(srcl);
+                const int nsrc = __popcll(SM);
+                if (nsrc <= 1) {
+                    res = true;
+                } else {
+                    if (srcl) ctl[kCtlSrc + count_below(SM)] = my_target;
+                    if (lane == 0) {
+                        ctl[kCtlCmd] = 1;
+                        ctl[kCtlVf] = (int)(pkf & 0x7fffu);
+                        ctl[kCtlA] = (int)((pkf >> 15) & 63u);
+                        ctl[kCtlNs] = nsrc;
+                    }
+                    block_sync();
+                    res = coop_bfs<RMAX>(G, a, bs, ctl, (int)threadIdx.x, (int)blockDim.x, bfs_levels);
+                }
+            } else {
+                res = wave_bfs<RMAX>(G, a, bs, lane, (int)(pkf & 0x7fffu), (int)((pkf >> 15) & 63u), my_target,
+                                     bfs_levels);
+            }
             FC_STAMP(t_b1);
             FC_PROF(13, t_b1 - t_b0);
             FC_PROF(14, 1);
@@ -785,6 +814,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         FC_PROF(4, t_e - t_d);
     }
     if (defer && qn > 0) wait_flush();
+    if (coop) {  // release the helper waves (every path of the chain's loop ends here)
+        if (lane == 0) ctl[kCtlCmd] = 0;
+        block_sync();
+    }
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
 #ifdef FC_PHASE_PROF
@@ -854,10 +887,11 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, siz
     // one chain (wave) per workgroup, as in fc_flip2.hip (C3 on one MI355X: 1.35e9 proposals/s
     // against 1.29e9 with four chains per workgroup); tune_chains_per_block = 2 / 4 restores larger ones
     const int wpb = p.wpb;  // fc_params.tune_chains_per_block (resolved by fc_run_create)
-    const int blocks = (p.n_chains + wpb - 1) / wpb;
-    const size_t lds = (size_t)p.chain_lds_bytes * wpb;
+    const int blocks = p.coop ? p.n_chains : (p.n_chains + wpb - 1) / wpb;
+    const size_t lds = (size_t)p.chain_lds_bytes * (p.coop ? 1 : wpb);
     hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(blocks), block(kWave * wpb);
+    // cooperative search: one chain per 256-thread workgroup (wave 0 + three search helpers)
+    const dim3 grid(blocks), block(p.coop ? kWave * kWavesPerBlock : kWave * wpb);
     // FULL: replay tapes, traces, event logs, histograms, per-node/per-edge tallies or a
     // hitting-time window; the lean instance (proposals, steps, sums, waits) keeps its
     // register budget for the hot loop.

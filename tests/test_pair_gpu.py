@@ -18,12 +18,13 @@ STAT_KEYS = ["steps", "proposals", "draws", "accepted", "inv_contig", "inv_pop",
 ALL_DIAG = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
 
 
-def _run_pair(spec, inits, bases, k, *, steps, pct, seed=21, flags=0, chunks=1, exact=True, proposal=None):
-    fg = FlipGraph(spec, exact=exact)
+def _run_pair(spec, inits, bases, k, *, steps, pct, seed=21, flags=0, chunks=1, exact=True, proposal=None,
+              use_positions=True, tune=None):
+    fg = FlipGraph(spec, exact=exact, use_positions=use_positions)
     _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
     cfg = RunConfig(k=k, labels=tuple(range(k)), proposal=_lib.FC_PROPOSE_PAIR if proposal is None else proposal,
                     seed=seed, pop_lo=lo, pop_hi=hi, diag_mask=ALL_DIAG, flags=flags,
-                    trace_chains=inits.shape[0], trace_cap=400000)
+                    trace_chains=inits.shape[0], trace_cap=400000, tune=tune)
     run = FlipRun(fg, inits, cfg, bases=bases)
     per = steps // chunks
     for i in range(chunks):
@@ -212,3 +213,28 @@ def test_tuning_fields_checked(gpu, sec11):
         cfg = RunConfig(**{**base.__dict__, "tune": bad})
         with pytest.raises(ValueError, match=what):
             FlipRun(fg, a4[None, :], cfg)
+
+
+@pytest.mark.parametrize("waves", [4, 1])
+@pytest.mark.parametrize("graph", ["delaunay10k", "triangular100"])
+def test_large_graph_search_workgroup_and_wave(gpu, cref, graph, waves):
+    """Large graphs given without positions (no planar rings, so neither the run rule's
+    exactness nor the district-graph rule): every multi-run proposal goes to the device search
+    -- by the whole 256-thread workgroup of the chain (tune_search_waves = 4) or by its one
+    wave (1, the default).  Both are bit-exact against the oracle's
+    BFS, per proposal, on C5's Delaunay graph (k = 18) and C4's triangular lattice (k = 8)."""
+    if graph == "delaunay10k":
+        spec = G.delaunay_graph(10000, seed=0)
+        k = 18
+        a0 = spec.assignment_array(G.bisection_plan(spec, k), list(range(k)))
+    else:
+        spec = G.triangular_graph(100, 198)
+        k = 8
+        a0 = spec.assignment_array(G.strip_plan(spec, k), list(range(k)))
+    inits = np.stack([a0] * 6)
+    bases = np.asarray([0.5, 1.0, 2.0] * 2)
+    run = _run_pair(spec, inits, bases, k, steps=400, pct=0.1, chunks=2, use_positions=False,
+                    tune={"search_waves": waves})
+    st = run.stats()
+    assert int(st["bfs_calls"].sum()) > 0
+    _check(cref, spec, run, k, inits, bases, steps=400, pct=0.1)

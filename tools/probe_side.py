@@ -13,13 +13,14 @@ from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, pa
 W = bench.Workload(sys.argv[1])
 S = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
 IT = int(sys.argv[4]) if len(sys.argv) > 4 else 2
-fg = FlipGraph(W.spec)
+# FC_PROBE_NOPOS=1: build the graph without positions (no planar rings); FC_PROBE_FLAGS: fc_params.flags
+fg = FlipGraph(W.spec, use_positions=os.environ.get("FC_PROBE_NOPOS", "0") != "1")
 C = (int(sys.argv[2]) if len(sys.argv) > 2 else 0) or (bench.resident_chains(fg, W) if W.name in ("c4", "c5")
                                                          else W.chains)
 inits = np.stack([W.init_of(g) for g in range(C)])
 bases = np.asarray([W.base_of(g) for g in range(C)])
 _, (lo, hi) = G.population_bounds(int(W.spec.pop.sum()), W.k, W.pct)
-run = FlipRun(fg, inits, RunConfig(tune=parse_tune(os.environ.get('FC_TUNE', '')), k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo,
+run = FlipRun(fg, inits, RunConfig(tune=parse_tune(os.environ.get('FC_TUNE', '')), flags=int(os.environ.get("FC_PROBE_FLAGS", "0")), k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo,
                                    pop_hi=hi), bases=bases)
 for it in range(IT):
     s0 = run.stats()
