@@ -30,7 +30,7 @@ EXPORTED = [
     "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
     "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_set_initial_wait", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
     "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_read_recom_trace",
-    "fc_run_trace_reset", "fc_run_read_hist",
+    "fc_run_trace_reset", "fc_run_read_hist", "fc_run_checkpoint", "fc_run_restore",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
     "fc_run_frame_series", "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
@@ -135,6 +135,8 @@ def load(build_if_missing: bool = True):
     L.fc_run_read_trace.argtypes = [vp, i32, _P(Record), i64, _P(i64)]
     L.fc_run_read_recom_trace.argtypes = [vp, i32, _P(RecomRecord), i64, _P(i64)]
     L.fc_run_trace_reset.argtypes = [vp]
+    L.fc_run_checkpoint.argtypes = [vp, ctypes.c_void_p, i64, _P(i64)]
+    L.fc_run_restore.argtypes = [vp, ctypes.c_void_p, i64]
     L.fc_run_read_hist.argtypes = [vp, _P(i64), _P(i64)]
     L.fc_run_read_edges.argtypes = [vp, _P(i64)]
     L.fc_run_read_flips.argtypes = [vp, _P(i64), _P(i64), _P(i64)]

@@ -809,6 +809,120 @@ int fc_run_timings(fc_run *r, float *ms, int32_t cap, int32_t *n) {
     return FC_OK;
 }
 
+namespace {
+
+struct CkptHeader {
+    char magic[8];          // "FCCKPT01"
+    int32_t n_chains, n, n_edges, k, ring_max, proposal, npad, dgraph;
+    uint32_t diag_mask;
+    int32_t reserved;
+    int64_t ev_cap, payload;
+};
+
+// (device pointer, bytes) of every buffer a checkpoint carries, in blob order
+std::vector<std::pair<void *, size_t>> ckpt_sections(fc_run *r) {
+    const size_t C = (size_t)r->n_chains, n = (size_t)r->g.n, E = (size_t)r->g.n_edges, k = (size_t)r->p.k;
+    const size_t R = (size_t)r->g.ring_max;
+    std::vector<std::pair<void *, size_t>> v;
+    v.emplace_back(r->d_assign, C * r->npad);
+    v.emplace_back(r->d_sc, C * sizeof(fc::ChainScalars));
+    if (r->p.proposal != FC_PROPOSE_RECOM) {
+        v.emplace_back(r->d_fcnt, C * r->npad);
+        v.emplace_back(r->d_popk, C * fc::kMaxKGeneral * 4);
+        v.emplace_back(r->d_thresh, C * (2 * R + 1) * 8);
+        if (r->dgraph) {
+            v.emplace_back(r->d_mcnt, C * k * k * 4);
+            v.emplace_back(r->d_ngk, C * 32 * 4);
+        }
+    }
+    if (r->d_cut_hist) v.emplace_back(r->d_cut_hist, C * (E + 1) * 8);
+    if (r->d_nb_hist) v.emplace_back(r->d_nb_hist, C * (n + 1) * 8);
+    if (r->d_edge_acc) v.emplace_back(r->d_edge_acc, C * E * 8);
+    if (r->d_num_flips) {
+        v.emplace_back(r->d_num_flips, C * n * 8);
+        v.emplace_back(r->d_part_sum, C * n * 8);
+        v.emplace_back(r->d_last_flipped, C * n * 8);
+    }
+    if (r->d_events) {
+        v.emplace_back(r->d_events, C * (size_t)r->ev_cap * sizeof(fc_event));
+        v.emplace_back(r->d_ser_a0, C * r->npad);
+    }
+    return v;
+}
+
+CkptHeader ckpt_header(const fc_run *r, int64_t payload) {
+    CkptHeader h{};
+    std::memcpy(h.magic, "FCCKPT01", 8);
+    h.n_chains = r->n_chains;
+    h.n = r->g.n;
+    h.n_edges = r->g.n_edges;
+    h.k = r->p.k;
+    h.ring_max = r->g.ring_max;
+    h.proposal = r->p.proposal;
+    h.npad = r->npad;
+    h.dgraph = r->dgraph ? 1 : 0;
+    h.diag_mask = r->p.diag_mask;
+    h.ev_cap = r->ev_cap;
+    h.payload = payload;
+    return h;
+}
+
+}  // namespace
+
+int fc_run_checkpoint(fc_run *r, void *buf, int64_t cap, int64_t *len) {
+    if (!r || !len) return fail(FC_ERR_ARG, "fc_run_checkpoint: null argument");
+    const auto secs = ckpt_sections(r);
+    int64_t payload = 0;
+    for (const auto &sc : secs) payload += (int64_t)sc.second;
+    const int64_t total = (int64_t)sizeof(CkptHeader) + payload;
+    *len = total;
+    if (!buf) return FC_OK;
+    if (cap < total) return fail(FC_ERR_ARG, "fc_run_checkpoint: buffer too small (" + std::to_string(total) + " bytes needed)");
+    if (int rc = fc_run_sync(r)) return rc;
+    const CkptHeader h = ckpt_header(r, payload);
+    unsigned char *out = (unsigned char *)buf;
+    std::memcpy(out, &h, sizeof h);
+    size_t off = sizeof h;
+    for (const auto &sc : secs) {
+        if (sc.second) HIP_TRY(hipMemcpy(out + off, sc.first, sc.second, hipMemcpyDeviceToHost));
+        off += sc.second;
+    }
+    return FC_OK;
+}
+
+int fc_run_restore(fc_run *r, const void *buf, int64_t len) {
+    if (!r || !buf) return fail(FC_ERR_ARG, "fc_run_restore: null argument");
+    if (len < (int64_t)sizeof(CkptHeader)) return fail(FC_ERR_ARG, "fc_run_restore: blob too short");
+    CkptHeader h;
+    std::memcpy(&h, buf, sizeof h);
+    const auto secs = ckpt_sections(r);
+    int64_t payload = 0;
+    for (const auto &sc : secs) payload += (int64_t)sc.second;
+    const CkptHeader want = ckpt_header(r, payload);
+    if (std::memcmp(h.magic, want.magic, 8) != 0) return fail(FC_ERR_ARG, "fc_run_restore: not a flipchain checkpoint");
+    if (h.n_chains != want.n_chains || h.n != want.n || h.n_edges != want.n_edges || h.k != want.k ||
+        h.ring_max != want.ring_max || h.proposal != want.proposal || h.npad != want.npad || h.dgraph != want.dgraph ||
+        h.diag_mask != want.diag_mask || h.ev_cap != want.ev_cap || h.payload != payload)
+        return fail(FC_ERR_ARG, "fc_run_restore: the checkpoint was taken from a run with another graph or fc_params");
+    if (len != (int64_t)sizeof(CkptHeader) + payload) return fail(FC_ERR_ARG, "fc_run_restore: blob size mismatch");
+    if (int rc = fc_run_sync(r)) return rc;
+    const unsigned char *in = (const unsigned char *)buf;
+    size_t off = sizeof h;
+    for (size_t i = 0; i < secs.size(); ++i) {
+        const auto &sc = secs[i];
+        if (i == 1) {  // ChainScalars: traces are outputs and restart empty
+            std::vector<fc::ChainScalars> s((size_t)r->n_chains);
+            std::memcpy(s.data(), in + off, sc.second);
+            for (auto &x : s) x.trace_len = 0;
+            HIP_TRY(hipMemcpy(sc.first, s.data(), sc.second, hipMemcpyHostToDevice));
+        } else if (sc.second) {
+            HIP_TRY(hipMemcpy(sc.first, in + off, sc.second, hipMemcpyHostToDevice));
+        }
+        off += sc.second;
+    }
+    return FC_OK;
+}
+
 int fc_run_read_stats(fc_run *r, fc_chain_stats *out) {
     if (!r || !out) return fail(FC_ERR_ARG, "fc_run_read_stats: null argument");
     if (int rc = fc_run_sync(r)) return rc;

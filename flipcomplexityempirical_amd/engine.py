@@ -220,6 +220,20 @@ class FlipRun:
         w = np.ascontiguousarray(words, dtype=np.uint32).reshape(self.n_chains, 2)
         check(_lib.load().fc_run_set_initial_wait(self.handle, _p(w, ctypes.c_uint32)), "fc_run_set_initial_wait")
 
+    def checkpoint(self) -> bytes:
+        """The run's resumable state as bytes (``fc_run_checkpoint``)."""
+        L = _lib.load()
+        n = ctypes.c_int64(0)
+        check(L.fc_run_checkpoint(self.handle, None, 0, ctypes.byref(n)), "fc_run_checkpoint")
+        buf = ctypes.create_string_buffer(int(n.value))
+        check(L.fc_run_checkpoint(self.handle, buf, n.value, ctypes.byref(n)), "fc_run_checkpoint")
+        return buf.raw
+
+    def restore(self, blob: bytes):
+        """Load a ``checkpoint()`` of a run with the same graph and configuration."""
+        buf = ctypes.create_string_buffer(bytes(blob), len(blob))
+        check(_lib.load().fc_run_restore(self.handle, buf, len(blob)), "fc_run_restore")
+
     def sync(self):
         check(_lib.load().fc_run_sync(self.handle))
 

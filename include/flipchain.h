@@ -288,6 +288,17 @@ int fc_run_autocorr(fc_run *r, const int32_t *lags, int32_t nlags, int64_t *lag_
 int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *frame_u,
                         const int32_t *frame_v, const double *mid_xy, double cx, double cy, int64_t cap,
                         double *slope, double *angle, int32_t *n_cut, int64_t *len);
+/* ---- checkpoint / resume ---------------------------------------------------- */
+/* Everything later fc_run_steps calls depend on -- every chain's assignment, foreign-neighbour
+ * counts, draw counter, counters and sums, populations, acceptance thresholds, district-graph
+ * tables, and the enabled per-yield accumulators (histograms, cut_times, flips, the series
+ * window and event log) -- as one byte blob.  fc_run_checkpoint with buf == NULL (or cap too
+ * small) stores the size in *len (FC_ERR_ARG when cap is too small).  fc_run_restore loads it
+ * into a run created with the same graph and fc_params (n_chains, k, proposal, diag_mask,
+ * event_cap are checked; FC_ERR_ARG otherwise); the chains then continue bit for bit as if
+ * never interrupted.  Per-proposal traces are outputs: they restart empty after a restore. */
+int fc_run_checkpoint(fc_run *r, void *buf, int64_t cap, int64_t *len);
+int fc_run_restore(fc_run *r, const void *buf, int64_t len);
 /* Name of the last launched flip-kernel instance, as rocprofv3 spells it. */
 int fc_run_kernel_name(const fc_run *r, char *buf, int32_t cap);
 int32_t fc_run_n_chains(const fc_run *r);
