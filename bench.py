@@ -323,18 +323,38 @@ def main():
         # cut / |B| histograms, per-edge cut_times, per-node num_flips / part_sum /
         # last_flipped), FULL instance; then the one §8(e) reduction of all of them
         run.close()
+        # the reference's slope / angle lines (:371-394) need the per-step interface: on sec11
+        # the kernel also logs every accepted flip, and after each launch the frame-series
+        # kernel turns the log into per-event slope / angle, copied to the host as the
+        # reference's lists (in chunks of chains)
+        series = args.workload == "c2"
         full = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
+        if series:
+            full |= _lib.FC_DIAG_SERIES
         cfg_f = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
-                          chain_id_offset=int(off), device=local_rank, diag_mask=full, tune=tune)
+                          chain_id_offset=int(off), device=local_rank, diag_mask=full, tune=tune,
+                          event_cap=args.chain_steps + 1 if series else 0)
         rf = FlipRun(fg, inits, cfg_f, bases=bases)
+        frame = G.slope_frame(spec, "sec11") if series else None
         rf.steps(args.chain_steps)
         barrier_sync_f = lambda: (rf.sync(), dist.barrier() if dist is not None else None)  # noqa: E731
+        if series:
+            rf.series_reset()
         barrier_sync_f()
         f0 = rf.stats()
         rf.timings()
+        t_series, n_events, n_nan = 0.0, 0, 0
         t0f = time.perf_counter()
         for _ in range(args.full_diag_steps):
             rf.steps(args.chain_steps)
+            if series:
+                ts = time.perf_counter()
+                for c0 in range(0, C, 256):
+                    fs = rf.frame_series(frame, chains=range(c0, min(C, c0 + 256)))
+                    n_events += int(fs["len"].sum())
+                    n_nan += int(np.isnan(fs["angle"]).sum())  # padding entries are 0, not NaN
+                rf.series_reset()
+                t_series += time.perf_counter() - ts
         barrier_sync_f()
         dtf = D.allreduce_max(time.perf_counter() - t0f, dist, dev)
         kf = D.allreduce_max(float(rf.timings().mean()), dist, dev)
@@ -347,10 +367,20 @@ def main():
         pf = float((f1["proposals"] - f0["proposals"]).sum())
         pf = float(D.allreduce_sum(np.asarray([pf]), dist, dev)[0])
         yields = int(red["scalars"][:, D.AGG_FIELDS.index("steps")].sum()) + C * world
-        full_out = {"value": pf / dtf, "unit": "proposals/s", "launches": args.full_diag_steps,
+        t_series = D.allreduce_max(t_series, dist, dev)
+        full_out = {"value": pf / (dtf - t_series), "unit": "proposals/s", "launches": args.full_diag_steps,
+                    "value_with_frame_series_on_host": pf / dtf if series else None,
                     "kernel": rf.kernel_name(), "kernel_ms": kf,
-                    "diag": "waits + cut/|B| histograms + per-edge cut_times + per-node flips "
-                            "(the reference loop body's tallies, grid_chain_sec11.py:367-400)",
+                    "diag": "waits + cut/|B| histograms + per-edge cut_times + per-node flips"
+                            + (" + accepted-flip log -> per-event slope / angle on the device, copied to "
+                               "the host" if series else "")
+                            + " (the reference loop body, grid_chain_sec11.py:367-400)",
+                    "frame_series": {"ms_per_launch": t_series / max(args.full_diag_steps, 1) * 1e3,
+                                     "events": n_events, "events_per_s": n_events / t_series if t_series else None,
+                                     "nan_angles": n_nan,
+                                     "note": "fc_run_frame_series over all chains in chunks of 256, per-event "
+                                             "slope / angle / frame-cut count copied to host arrays"}
+                    if series else None,
                     "reduced": {"ranks": world, "collectives": "allreduce SUM (scalars, histograms, cut_times, "
                                 "num_flips, part_sum) + allreduce MAX (last_flipped)",
                                 "yields": yields, "cut_hist_mass": int(red["cut_hist"].sum()),
