@@ -348,6 +348,7 @@ def main():
         for _ in range(args.full_diag_steps):
             rf.steps(args.chain_steps)
             if series:
+                rf.sync()  # the launch is asynchronous: its time must not land in t_series
                 ts = time.perf_counter()
                 for c0 in range(0, C, 256):
                     fs = rf.frame_series(frame, chains=range(c0, min(C, c0 + 256)))
