@@ -59,7 +59,8 @@ class Params(ctypes.Structure):
                 ("tune_nsub", ctypes.c_int32), ("tune_hit_stop", ctypes.c_int32),
                 ("tune_par_min", ctypes.c_int32), ("tune_wait_queue", ctypes.c_int32),
                 ("tune_chains_per_block", ctypes.c_int32), ("tune_prio_div", ctypes.c_int32 * 3),
-                ("tune_prio_th", ctypes.c_float * 3), ("tune_search_waves", ctypes.c_int32)]
+                ("tune_prio_th", ctypes.c_float * 3), ("tune_search_waves", ctypes.c_int32),
+                ("tune_deal", ctypes.c_int32)]
 
 
 class ChainStats(ctypes.Structure):

@@ -16,8 +16,8 @@ CSRC = os.path.join(PKG, "csrc")
 VARIANT = os.environ.get("FC_LIB_VARIANT", "")
 VARIANT_FLAGS = {"prof": "-DFC_PHASE_PROF", "sync": "-DFC_PHASE_SYNC"}
 LIB = os.environ.get("FC_LIB_OUT") or os.path.join(PKG, f"libflipchain_{VARIANT}.so" if VARIANT else "libflipchain.so")
-SOURCES = ["fc_flip2.hip", "fc_kernels.hip", "fc_series.hip", "fc_recom.hip", "fc_capi.cpp", "fc_graph.cpp"]
-HEADERS = ["fc_internal.h", "fc_philox.h", "fc_device.h", os.path.join("..", "..", "include", "flipchain.h")]
+SOURCES = ["fc_flip2.hip", "fc_deal.hip", "fc_kernels.hip", "fc_series.hip", "fc_recom.hip", "fc_capi.cpp", "fc_graph.cpp"]
+HEADERS = ["fc_internal.h", "fc_philox.h", "fc_device.h", "fc_ring.h", os.path.join("..", "..", "include", "flipchain.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("FC_OFFLOAD_ARCH", "gfx950")
 

@@ -56,6 +56,8 @@ struct fc_run {
     int64_t tape_draws = 0;
     int64_t *d_prof = nullptr;  // FC_PHASE_PROF builds
     uint32_t *d_eta = nullptr;  // k = 2: per-launch pace of the slowest chain (issue priorities)
+    uint32_t *d_deal = nullptr, *d_order = nullptr, *d_ctime = nullptr;  // k = 2 chain dealing (fc_deal.hip)
+    bool deal_timed = false;    // d_ctime holds a launch's per-chain durations
     int64_t n_flip_launches = 0;
     int32_t *d_eu = nullptr, *d_ev = nullptr;  // recom: canonical edge list
     uint64_t *d_recom_thresh = nullptr;        // recom: [2E+1] acceptance thresholds
@@ -63,7 +65,7 @@ struct fc_run {
     char kname[96] = {0};        // last launched flip-kernel instance
     bool variant = false;        // accept / constraint variants (FULL k = 2 instance)
     struct {                     // fc_params.tune_* with the defaults filled in
-        int32_t nsub, hit_stop, par_min, wait_q, wpb, coop;
+        int32_t nsub, hit_stop, par_min, wait_q, wpb, coop, deal;
         int32_t prio_div[3];     // prio_div[0] <= 0: priorities off
         float prio_th[3];
     } tune{};
@@ -100,7 +102,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -362,6 +364,12 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         for (int i = 0; i < 3; ++i) t.prio_div[i] = div_default ? (i == 0 ? 2 : i == 1 ? 5 : 10) : p->tune_prio_div[i];
         if (t.prio_div[0] > 0 && (t.prio_div[1] <= 0 || t.prio_div[2] <= 0))
             return fail(FC_ERR_ARG, "fc_run_create: tune_prio_div needs three positive divisors (or [0] < 0: off)");
+        // k = 2: deal chains to SIMDs by the previous launch's draws (fc_deal.hip).  Off by
+        // default: C2's dispatch order already gives every SIMD one or two of its slow chains
+        // (chain dealing)
+        t.deal = p->tune_deal ? p->tune_deal : -1;
+        if (t.deal != 1 && t.deal != -1) return fail(FC_ERR_ARG, "fc_run_create: tune_deal must be 1 or -1");
+        t.deal = t.deal > 0 && k == 2 && !recom;
         const bool th_default = p->tune_prio_th[0] == 0.0f && p->tune_prio_th[1] == 0.0f && p->tune_prio_th[2] == 0.0f;
         const float th0[3] = {0.9f, 1.0f, 1.1f};
         for (int i = 0; i < 3; ++i) t.prio_th[i] = th_default ? th0[i] : p->tune_prio_th[i];
@@ -747,9 +755,28 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
         }
         k.eta = r->d_eta;
     }
+    k.deal = nullptr;
+    k.order = nullptr;
+    k.ctime = nullptr;
+    if (r->tune.deal) {
+        if (!r->d_deal) {
+            if (int rc = dalloc(&r->d_deal, (size_t)fc::kDealKeys + 4)) return rc;
+            if (int rc = dalloc(&r->d_order, (size_t)r->n_chains)) return rc;
+            if (int rc = dalloc(&r->d_ctime, (size_t)r->n_chains)) return rc;
+        }
+        k.deal = r->d_deal;
+        k.order = r->d_order;
+        k.ctime = r->d_ctime;
+    }
     for (int64_t done = 0; done < n_steps; done += kChunk) {
         k.n_steps = std::min(kChunk, n_steps - done);
         if (max_draws <= 0) k.max_draws = 65536 * k.n_steps;
+        if (k.order) {  // this launch's deal: chains by the last one's durations (first: by |B|)
+            const int e = fc::launch_deal_order(r->d_ctime, r->d_sc, k.n, r->n_chains, r->deal_timed ? 1 : 0,
+                                                r->d_order, r->d_deal, s);
+            if (e != 0) return fail(FC_ERR_HIP, std::string("deal kernel launch: ") + hipGetErrorString((hipError_t)e));
+            r->deal_timed = true;
+        }
         if (k.eta) {
             k.eta_parity = (int32_t)(r->n_flip_launches++ & 1);
             HIP_TRY(hipMemsetAsync(r->d_eta + k.eta_parity, 0, sizeof(uint32_t), s));
@@ -820,7 +847,7 @@ struct CkptHeader {
 };
 
 // (device pointer, bytes) of every buffer a checkpoint carries, in blob order
-std::vector<std::pair<void *, size_t>> ckpt_sections(fc_run *r) {
+static std::vector<std::pair<void *, size_t>> ckpt_sections(fc_run *r) {
     const size_t C = (size_t)r->n_chains, n = (size_t)r->g.n, E = (size_t)r->g.n_edges, k = (size_t)r->p.k;
     const size_t R = (size_t)r->g.ring_max;
     std::vector<std::pair<void *, size_t>> v;
@@ -920,6 +947,7 @@ int fc_run_restore(fc_run *r, const void *buf, int64_t len) {
         }
         off += sc.second;
     }
+    r->deal_timed = false;  // the restored chains' pace is not the last launch's
     return FC_OK;
 }
 

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "fc_internal.h"
+#include "fc_ring.h"
 
 namespace fc {
 namespace dev {
@@ -68,22 +69,33 @@ __device__ __forceinline__ int ring_entry(const uint32_t (&ring)[RMAX / 2], int 
     return (int)((ring[i >> 1] >> (16 * (i & 1))) & 0xffffu);
 }
 
-// At most one of the cyclic intervals between consecutive old-district neighbours holds a
-// break (a ring step that is not an old-district link) <=> the neighbours form one run.
-__device__ __forceinline__ bool one_run(uint32_t nbrA, uint32_t brk, uint32_t full) {
-    if (__popc(nbrA) <= 1) return true;
-    uint32_t cur = nbrA & (0u - nbrA);
-    uint32_t rest = nbrA & (nbrA - 1u);
-    int cnt = 0;
-    while (rest) {
-        const uint32_t nx = rest & (0u - rest);
-        cnt += (brk & (nx - cur)) != 0u;
-        cur = nx;
-        rest &= rest - 1u;
+using fc::one_run;  // fc_ring.h
+
+// Chain dealing (fc_deal.hip): the chain this wave runs.  Lane 0 reads the wave's SIMD
+// (HW_ID: SIMD, pipe, CU, SH, SE; XCC_ID: the XCD), takes the next arrival slot s on that
+// SIMD and claims the next chain of quarter s of p.order (slowest quarter first), falling
+// through to the following quarters when one is used up: the claims are a bijection of the
+// launch's waves onto its chains whatever the placement.  Vector atomics only.
+__device__ __forceinline__ int deal_chain(const KParams &p, int lane) {
+    int cc = 0;
+    if (lane == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const uint32_t key = ((xcc & 7u) << 12) | ((hw >> 4) & 0xfffu);
+        const uint32_t slot = atomicAdd(&p.deal[key], 1u);
+        const uint32_t C = (uint32_t)p.n_chains;
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t q = (slot + k) & 3u;
+            const uint32_t lo = q * C / 4u, hi = (q + 1u) * C / 4u;
+            const uint32_t i = atomicAdd(&p.deal[kDealKeys + q], 1u);
+            if (lo + i < hi) {
+                cc = (int)p.order[lo + i];
+                break;
+            }
+        }
     }
-    const uint32_t first = nbrA & (0u - nbrA);  // wrap interval [cur, L) U [0, first)
-    cnt += (brk & ((full & ~(cur - 1u)) | (first - 1u))) != 0u;
-    return cnt <= 1;
+    return __builtin_amdgcn_readfirstlane(__shfl(cc, 0));
 }
 
 // BFS scratch of one chain (LDS): the source label of every visited node (one byte:

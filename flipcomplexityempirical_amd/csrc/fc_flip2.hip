@@ -41,8 +41,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int c = (int)blockIdx.x * (int)(blockDim.x >> 6) + wv;
-    if (c >= p.n_chains) return;
+    const int wave = (int)blockIdx.x * (int)(blockDim.x >> 6) + wv;
+    if (wave >= p.n_chains) return;
+    const int c = p.order ? deal_chain(p, lane) : wave;  // chain dealing (fc_deal.hip)
 
     const int n = p.n;
     const int npad = (n + 15) & ~15;
@@ -108,6 +109,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     if (lane < kProfSlots) prof_acc[lane] = 0;
 #endif
     wave_sync();
+#ifdef FC_PHASE_PROF
+    {  // slot 20: the wave's SIMD (XCC_ID . HW_ID[15:4], as deal_chain keys it)
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        FC_PROF(20, (int64_t)(((xcc & 7u) << 12) | ((hw >> 4) & 0xfffu)));
+    }
+#endif
     FC_STAMP(t_loop0);
 
     // issue priority among the waves sharing a SIMD (scheduling only: trajectories are
@@ -182,7 +191,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + (inrange ? dr : draw)) * 6;
                 w = Words4{t[0], t[1], t[2], t[3]};
             } else {
+#ifdef FC_EXP_CHEAPRNG
+                {  // timing experiment only: a 2-multiply mix instead of Philox (not the canonical stream)
+                    uint64_t z = dr * 0x9E3779B97F4A7C15ull + ((uint64_t)chain_gid << 32) + p.seed_lo;
+                    z = (z ^ (z >> 31)) * 0xBF58476D1CE4E5B9ull;
+                    z ^= z >> 29;
+                    w = Words4{(uint32_t)z, (uint32_t)(z >> 32), (uint32_t)(z >> 16) ^ (uint32_t)dr, 0u};
+                }
+#else
                 w = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
+#endif
             }
             const uint64_t m = (uint64_t)w.x0 * (uint64_t)(uint32_t)n;
             const int vd = (int)(m >> 32);
@@ -280,6 +298,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // the one-draw-at-a-time chain.  The commit marks of the segment passes so far are
         // cleared first: every slot's view is current again.
         auto reeval = [&](int from) {
+            FC_STAMP(t_re0);
             if (st & LF_WROTE) {
                 smark[v] = 0xff;
 #pragma unroll
@@ -310,6 +329,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                      (sl ? LF_SLIN : 0u) | (sc ? LF_SCYC : 0u);
             }
             compiler_fence();
+            FC_STAMP(t_re1);
+            FC_PROF(16, t_re1 - t_re0);
+            FC_PROF(17, 1);
         };
 
         // contiguity undecided by the ring rule at lane f: wave BFS on the current state
@@ -338,25 +360,20 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const bool hit = (st & LF_HIT) != 0, acc = (st & LF_ACC) != 0, s_lin = (st & LF_SLIN) != 0,
                        s_cyc = (st & LF_SCYC) != 0, exact = (st & LF_EXACT) != 0, gam = (st & LF_GAM) != 0,
                        has = (st & LF_HAS) != 0;
-            const bool prop = hit && lane >= pos && lane < end;
+            const bool prop = hit & (lane >= pos) & (lane < end);
             // contiguity verdict when the other district does (okT) / does not (okN) touch
             // the outer face -- the outer-face counts are chain-global
-            bool known = true, okT, okN;
-            if (st & ST_BD) {
-                okT = okN = (st & ST_BR) != 0;
-            } else if (nA == 0) {
-                okT = okN = false;
-            } else if (exact) {
-                okT = s_lin;
-                okN = gam ? s_cyc : s_lin;
-            } else {
-                known = s_lin;
-                okT = okN = s_lin;
-            }
+            // (selects, not an if-chain: the chain compiled to nested exec-mask branches)
+            // BFS verdict if any; no old-district neighbour: invalid; else the run rule, exact
+            // or (not exact) deciding only "one run"
+            const bool bd = (st & ST_BD) != 0, br = (st & ST_BR) != 0, nz = nA != 0;
+            const bool okT = bd ? br : (nz & s_lin);
+            const bool okN = bd ? br : (nz & ((exact & gam) ? s_cyc : s_lin));
+            const bool known = bd | !nz | exact | s_lin;
             const bool ok = ((av ? ng0 : ng1) > 0) ? okT : okN;
             const int pa = av ? pops1 : pops0, pb = av ? pops0 : pops1;
             const bool popok = (pa - pv >= p.pop_lo) && (pb + pv <= p.pop_hi);
-            bool valid = prop && known && ok && popok;
+            bool valid = prop & known & ok & popok;
             bool acc_now = acc;
             bool inv_contig = !ok;  // reason of an invalid proposal: contiguity, else "pop"
             if constexpr (FULL) {
@@ -462,6 +479,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         need = need && again;
                         if (!__any(need)) break;
                     }
+                    FC_STAMP(t_mk);
+                    FC_PROF(18, t_mk - t_it1);
                     // alpha (later slots), entering non-hits and beta (later candidates)
                     bool conf = has && ms < lane;
 #pragma unroll
@@ -494,6 +513,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         FC_PROF(14, 1);
                     }
                 }
+                FC_STAMP(t_cf);
+                FC_PROF(19, t_cf - t_it1);
                 const int ce = min(sg, x);  // commit lanes [pos, ce)
                 if (x < sg) last_step = false;
                 if (prop && lane < ce) st |= valid1 ? (cand1 ? (ST_VS | ST_AC) : ST_VS) : (ok1 ? ST_IP : ST_IC);
@@ -618,17 +639,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             uint64_t ent = __ballot(enter);
             const int dnb = __popcll(ent) - __popcll(__ballot(leave));
             // non-hit draws after f whose node just entered the boundary would now propose
+            // (the counts written above are read back: a non-hit node had no foreign neighbour
+            // when it was drawn, and a flip before f that gave it one has cut the batch already)
             if (ent) {
                 const int off_f = rl32(off_l, f);
                 int t_na = trunc_off;
-                while (ent) {
-                    const int un = rl32(my_e, __builtin_ctzll(ent));
-                    ent &= ent - 1;
 #pragma unroll
-                    for (int r = 0; r < NSUB; ++r) {
-                        const uint64_t m2 = __ballot(rv[r] == un && 64 * r + lane > off_f);
-                        if (m2) t_na = min(t_na, 64 * r + __builtin_ctzll(m2));
-                    }
+                for (int r = 0; r < NSUB; ++r) {
+                    const bool tr = (rv[r] >= 0) & (64 * r + lane > off_f) && fcnt[rv[r] < 0 ? 0 : rv[r]] != 0;
+                    const uint64_t m2 = __ballot(tr);
+                    if (m2) t_na = min(t_na, 64 * r + __builtin_ctzll(m2));
                 }
                 if (t_na < trunc_off) {
                     trunc_off = t_na;
@@ -848,6 +868,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     if (defer && qn > 0) wait_flush();
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
+#ifdef FC_EXP_DEAL_TIME
+    if (p.ctime && lane == 0) p.ctime[c] = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - rt0, (uint64_t)0xffffffffu);
+#else
+    // the chain's own work this launch (draws: a short boundary costs many per step), not its
+    // duration, which its SIMD-mates stretch
+    if (p.ctime && lane == 0) p.ctime[c] = (uint32_t)min(draw - scp->draw, (uint64_t)0xffffffffu);
+#endif
     if (p.eta && rem == 0 && lane == 0) {  // this launch's pace, for the next one's priorities
         const uint64_t el = __builtin_amdgcn_s_memrealtime() - rt0;
         atomicMax(&p.eta[p.eta_parity], (uint32_t)min(el * 1024ull / (uint64_t)max((int)p.n_steps, 1), 0xffffffffull));

@@ -140,13 +140,23 @@ struct KParams {
     int32_t *ngk;               // [n_chains * 32] outer-face nodes per district
     int32_t coop;               // k > 2 large graphs without the district rule: one chain per
                                 // 256-thread workgroup, contiguity searches by the whole workgroup
+    // chain dealing (k = 2): a wave takes its chain by its arrival slot on its SIMD, from the
+    // slot's quarter of `order` (chains by the previous launch's duration, slowest first), so
+    // that every SIMD runs one chain of each quarter instead of whatever the dispatcher's
+    // order piles onto it (fc_deal.hip)
+    uint32_t *deal;             // [kDealKeys + 4]: arrivals per SIMD key, claims per quarter (zeroed per launch)
+    const uint32_t *order;      // [n_chains] chain ids, slowest first (null: no dealing)
+    uint32_t *ctime;            // [n_chains] draws each chain took in its last launch (the dealing key)
 };
+
+// chain dealing: SIMD keys are XCC_ID[2:0] . HW_ID[15:4] (SIMD, pipe, CU, SH, SE)
+constexpr int kDealKeys = 1 << 15;
 
 // Diagnostic build (-DFC_PHASE_PROF): s_memtime cycles per kernel phase, per chain.
 // slots: 0 loop total, 1 draws, 2 evaluate, 3 commit, 4 bookkeeping, 5 batches,
 //        6 commit-loop iterations, 7 applied flips; k = 2 commit detail: 8 verdicts,
 //        9 one-event classify, 10 one-event apply, 11 segment-parallel, 12 segments
-constexpr int kProfSlots = 16;
+constexpr int kProfSlots = 24;
 // k = 2 lean kernel: accepted states queued for their geometric wait (fc_flip2.hip wait_flush)
 constexpr int kWaitQ = 64;
 // k > 2 kernel: 32 entries, so that sec11 chains keep four waves per SIMD in 160 KB of LDS
@@ -177,7 +187,11 @@ int launch_recom(const RecomParams &p, int ring_max, void *stream, char *name, s
 // `name` (may be null) receives the launched instance, spelled as rocprofv3 reports it.
 int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap);  // k > 2
 int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap);    // k = 2
-int launch_init_fcnt(const KParams &p, int ring_max, void *stream);
+// chain dealing (fc_deal.hip): order[] = chains by descending key (ctime, the last launch's
+// draws, if `timed`, else the boundary length's complement n - |B|: a short boundary needs
+// many draws per proposal), and the deal counters zeroed, for the next flip launch
+int launch_deal_order(const uint32_t *ctime, const ChainScalars *sc, int n, int n_chains, int timed,
+                      uint32_t *order, uint32_t *deal, void *stream);
 
 // Series diagnostics (fc_series.hip): expand the event logs of chains [c0, c0 + nc) into
 // dense |cut| series x[(c - c0) * stride + t], t < len[c], then accumulate per lag

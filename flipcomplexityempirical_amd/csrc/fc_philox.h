@@ -26,6 +26,12 @@ FC_HD Words4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, u
         if (r) {
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
+#if defined(__HIP_DEVICE_COMPILE__)
+            // keep the key schedule two scalar adds per round: hoisted out of the kernels'
+            // loops, its 20 round keys were held in SGPRs, spilled to VGPR lanes and reloaded
+            // (v_readlane + hazard nop) in every round
+            asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
         }
         // one v_mad_u64_u32 per product gives both halves
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;

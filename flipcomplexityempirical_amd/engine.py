@@ -119,12 +119,12 @@ class RunConfig:
     recom_max_attempts: int = 0
     # launch tuning (fc_params.tune_*): scheduling only, never the trajectory; 0 = default.
     # Keys: nsub, hit_stop, par_min, wait_queue, chains_per_block, prio_div (3), prio_th (3),
-    # search_waves.
+    # search_waves, deal.
     tune: Optional[Dict[str, object]] = None
 
 
 TUNE_KEYS = ("nsub", "hit_stop", "par_min", "wait_queue", "chains_per_block", "prio_div", "prio_th",
-             "search_waves")
+             "search_waves", "deal")
 
 
 def parse_tune(text: str) -> Dict[str, object]:

@@ -147,6 +147,10 @@ typedef struct fc_params {
                                    256-thread workgroup, searches by the whole workgroup;
                                    1 = one-wave workgroups, wave search (default: faster on
                                    the short searches of C4 / C5)                */
+    int32_t tune_deal;          /* k = 2 chain dealing: each SIMD runs one chain of every quarter
+                                   of the previous launch's draws (most first) instead of the
+                                   dispatcher's order; 1 = on, -1 = off (default).  Changes
+                                   which wave runs which chain, never a trajectory              */
 } fc_params;
 
 /* Per-chain statistics.  "Yields" are the states a `for part in exp_chain` loop sees:

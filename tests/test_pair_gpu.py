@@ -209,7 +209,7 @@ def test_tuning_fields_checked(gpu, sec11):
     _, (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 4, 0.05)
     base = RunConfig(k=4, labels=tuple(range(4)), proposal=_lib.FC_PROPOSE_PAIR, seed=1, pop_lo=lo, pop_hi=hi)
     for bad, what in (({"nsub": 3}, "k > 2"), ({"wait_queue": 33}, "tune_wait_queue"),
-                      ({"chains_per_block": 3}, "tune_chains_per_block")):
+                      ({"chains_per_block": 3}, "tune_chains_per_block"), ({"deal": 2}, "tune_deal")):
         cfg = RunConfig(**{**base.__dict__, "tune": bad})
         with pytest.raises(ValueError, match=what):
             FlipRun(fg, a4[None, :], cfg)

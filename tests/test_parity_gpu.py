@@ -180,14 +180,14 @@ def test_sharded_equals_unsharded(gpu, sec11):
 @pytest.mark.parametrize("nsub,hit_stop,extra", [(1, 64, {}), (2, 32, {}), (4, 12, {}), (4, 32, {}), (4, 64, {}),
                                                (4, 32, {"wait_queue": 1}), (4, 32, {"wait_queue": 3}),
                                                (4, 32, {"par_min": 65}), (4, 32, {"par_min": 1}),
-                                               (4, 32, {"chains_per_block": 4}),
+                                               (4, 32, {"chains_per_block": 4}), (4, 32, {"deal": 1}),
                                                (4, 32, {"prio_div": (-1, 0, 0)}),
                                                (2, 32, {"prio_th": (-1.0, 0.0, 0.0)})])
 @pytest.mark.parametrize("lean", [True, False])
 def test_sec11_batch_shapes(gpu, cref, sec11, nsub, hit_stop, extra, lean):
     """Every launch-tuning field of fc_params (draw rounds per batch ``tune_nsub``, the round
     cut-off ``tune_hit_stop``, the deferred-wait queue length, the segment-parallel threshold,
-    chains per workgroup, issue priorities) is a scheduling choice only: the lean instance
+    chains per workgroup, issue priorities, chain dealing) is a scheduling choice only: the lean instance
     (waits only) and the full instance (trace + histograms) stay bit-exact against the oracle
     under each of them (the guarantee include/flipchain.h states for fc_params.tune_*)."""
     inits, bases = _configs(sec11, G.sec11_plan, G.SEC11_BASES, 30)
