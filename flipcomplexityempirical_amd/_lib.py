@@ -22,6 +22,7 @@ FC_ERR_NOMEM = -5
 FC_GRAPH_NO_EXACT = 0x1
 FC_PROPOSE_BI_SIGN, FC_PROPOSE_PAIR, FC_PROPOSE_RECOM = 0, 1, 2
 FC_DIAG_WAIT, FC_DIAG_HIST, FC_DIAG_EDGES, FC_DIAG_FLIPS, FC_DIAG_SERIES = 0x1, 0x2, 0x4, 0x8, 0x10
+FC_DIAG_FLIPS_EXACT = 0x20
 FC_FLAG_FORCE_BFS = 0x1
 FC_ACCEPT_CUT, FC_ACCEPT_UNIFORM, FC_ACCEPT_ANNEAL = 0, 1, 2
 FC_CON_CONTIG, FC_CON_POP, FC_CON_BOUNDARY, FC_CON_FIXED, FC_CON_EMPTY = 0x1, 0x2, 0x4, 0x8, 0x100
@@ -31,7 +32,8 @@ EXPORTED = [
     "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_set_initial_wait", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
     "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_read_recom_trace",
     "fc_run_trace_reset", "fc_run_read_hist", "fc_run_checkpoint", "fc_run_restore",
-    "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
+    "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_flips_exact", "fc_run_read_wait_expected",
+    "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
     "fc_run_frame_series", "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
 ]
@@ -141,6 +143,8 @@ def load(build_if_missing: bool = True):
     L.fc_run_read_hist.argtypes = [vp, _P(i64), _P(i64)]
     L.fc_run_read_edges.argtypes = [vp, _P(i64)]
     L.fc_run_read_flips.argtypes = [vp, _P(i64), _P(i64), _P(i64)]
+    L.fc_run_read_flips_exact.argtypes = [vp, _P(i64), _P(i64), _P(i64)]
+    L.fc_run_read_wait_expected.argtypes = [vp, _P(dbl)]
     L.fc_run_read_events.argtypes = [vp, i32, _P(Event), i64, _P(i64)]
     L.fc_run_series_reset.argtypes = [vp]
     L.fc_run_autocorr.argtypes = [vp, _P(i32), i32, _P(i64), _P(dbl)]

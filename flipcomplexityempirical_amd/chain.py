@@ -669,14 +669,17 @@ class MarkovChain:
         run.close()
 
     # ---- fast path -------------------------------------------------------------------
-    def run(self, series: bool = True, frame: Optional[str] = "auto") -> "ChainResult":
+    def run(self, series: bool = True, frame: Optional[str] = "auto", corrected: bool = True) -> "ChainResult":
         """All ``total_steps`` yields on the device; the reference driver's outputs
         (``grid_chain_sec11.py:366-419``) come back as a :class:`ChainResult`.
 
         ``series`` keeps the per-yield lists ``rce`` / ``rbn`` (``:367-369``) through the
         device event log; ``frame`` ("sec11", "frank", None or "auto": from the
         ``slope`` updater and the node labels) adds the ``slopes`` / ``angles`` lists
-        (``:371-394``) computed by ``fc_run_frame_series``."""
+        (``:371-394``) computed by ``fc_run_frame_series``.  ``corrected`` adds the
+        statistics the driver's quirky tallies aim at, beside them:
+        ``flip_count`` / ``occupancy`` / ``last_accept`` (FC_DIAG_FLIPS_EXACT) and the
+        Rao-Blackwellised ``waits_expected``."""
         if self.cspec.proposal == _lib.FC_PROPOSE_RECOM:
             return self._run_recom()
         diag = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
@@ -687,10 +690,19 @@ class MarkovChain:
                 frame = "frank" if neg else "sec11"
         if series:
             diag |= _lib.FC_DIAG_SERIES
+        if corrected:
+            diag |= _lib.FC_DIAG_FLIPS_EXACT
         run = self._make_run(trace=False, diag=diag, event_cap=max(self.total_steps, 1) if series else 0)
         if self.total_steps > 1:
             run.steps(self.total_steps - 1)
         res = ChainResult.from_run(self, run, 0)
+        if corrected:
+            sp = self.cspec.spec
+            xf, xo, xl = run.flips_exact()
+            res.flip_count = {sp.nodes[i]: int(xf[0, i]) for i in range(sp.n)}
+            res.occupancy = {sp.nodes[i]: int(xo[0, i]) for i in range(sp.n)}
+            res.last_accept = {sp.nodes[i]: int(xl[0, i]) for i in range(sp.n)}
+            res.waits_expected = float(run.wait_expected()[0])
         if series:
             res.rce = run.yield_values("cut", 0)
             res.rbn = run.yield_values("nb", 0)
@@ -737,6 +749,11 @@ class ChainResult:
     rbn: Optional[np.ndarray] = None     # per-yield len(b_nodes)     (:369)
     slopes: Optional[np.ndarray] = None  # per-yield slope            (:371-382)
     angles: Optional[np.ndarray] = None  # per-yield angle            (:389-394)
+    # corrected companions of the quirky tallies (run(corrected=True)):
+    flip_count: Optional[Dict[Hashable, int]] = None   # accepted flips (num_flips counts re-yields)
+    occupancy: Optional[Dict[Hashable, int]] = None    # sum_t label (part_sum lacks final segments)
+    last_accept: Optional[Dict[Hashable, int]] = None  # yield of the last accepted flip
+    waits_expected: Optional[float] = None             # sum_t E[geom | |B_t|] (cached-sample-free)
 
     def heatmaps(self, shape=(40, 40), offset=(0, 0)) -> Dict[str, np.ndarray]:
         """The driver's ``A2`` arrays (``grid_chain_sec11.py:431-528``): ``A2[n[0], n[1]]``

@@ -45,6 +45,7 @@ struct fc_run {
     int64_t *d_cut_hist = nullptr, *d_nb_hist = nullptr;
     int64_t *d_edge_acc = nullptr;
     int64_t *d_num_flips = nullptr, *d_part_sum = nullptr, *d_last_flipped = nullptr;
+    int64_t *d_flip_count = nullptr, *d_occ_acc = nullptr, *d_last_accept = nullptr;  // FC_DIAG_FLIPS_EXACT
     int32_t *d_popk = nullptr;
     int32_t *d_mcnt = nullptr, *d_ngk = nullptr;  // k > 2 district-graph rule tables
     bool dgraph = false;
@@ -102,7 +103,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_trace, r->d_tape, r->d_popk, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -542,6 +543,13 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         HIP_TRY(hipMemset(r->d_last_flipped, 0, (size_t)n_chains * n * 8));
         HIP_TRY(hipMemcpy(r->d_part_sum, part_sum.data(), part_sum.size() * 8, hipMemcpyHostToDevice));
     }
+    if (p->diag_mask & FC_DIAG_FLIPS_EXACT) {
+        if (recom) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: FC_DIAG_FLIPS_EXACT is kept by the flip kernels, not ReCom");
+        for (int64_t **b : {&r->d_flip_count, &r->d_occ_acc, &r->d_last_accept}) {
+            if ((rc = dalloc(b, (size_t)n_chains * n))) return rc;
+            HIP_TRY(hipMemset(*b, 0, (size_t)n_chains * n * 8));
+        }
+    }
     if ((p->diag_mask & FC_DIAG_SERIES) && p->event_cap > 0) {
         if (E > 65535) return fail(FC_ERR_UNSUPPORTED, "fc_run_create: FC_DIAG_SERIES stores |cut| in 16 bits (E <= 65535)");
         r->ev_cap = p->event_cap;
@@ -656,6 +664,9 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.num_flips = r->d_num_flips;
     k.part_sum = r->d_part_sum;
     k.last_flipped = r->d_last_flipped;
+    k.flip_count = r->d_flip_count;
+    k.occ_acc = r->d_occ_acc;
+    k.last_accept = r->d_last_accept;
     k.trace = r->d_trace;
     k.trace_chains = r->p.trace_chains;
     k.trace_cap = r->p.trace_cap;
@@ -869,6 +880,11 @@ static std::vector<std::pair<void *, size_t>> ckpt_sections(fc_run *r) {
         v.emplace_back(r->d_num_flips, C * n * 8);
         v.emplace_back(r->d_part_sum, C * n * 8);
         v.emplace_back(r->d_last_flipped, C * n * 8);
+    }
+    if (r->d_flip_count) {
+        v.emplace_back(r->d_flip_count, C * n * 8);
+        v.emplace_back(r->d_occ_acc, C * n * 8);
+        v.emplace_back(r->d_last_accept, C * n * 8);
     }
     if (r->d_events) {
         v.emplace_back(r->d_events, C * (size_t)r->ev_cap * sizeof(fc_event));
@@ -1318,6 +1334,44 @@ int fc_run_read_flips(fc_run *r, int64_t *num_flips, int64_t *part_sum, int64_t 
             if (r->p.k == 2 && t_r != 0) part_sum[c * n + u] += (lab - lsum) * t_r;
             if (t_r == 0) part_sum[c * n + u] = T * lab;  // grid_chain_sec11.py:416-418
         }
+    }
+    return FC_OK;
+}
+
+int fc_run_read_flips_exact(fc_run *r, int64_t *flip_count, int64_t *occupancy, int64_t *last_accept) {
+    if (!r || !flip_count || !occupancy || !last_accept) return fail(FC_ERR_ARG, "fc_run_read_flips_exact: null argument");
+    if (!r->d_flip_count) return fail(FC_ERR_ARG, "fc_run_read_flips_exact: FC_DIAG_FLIPS_EXACT not enabled");
+    if (int rc = fc_run_sync(r)) return rc;
+    const size_t n = r->g.n, C = r->n_chains;
+    std::vector<int8_t> a(C * r->npad);
+    std::vector<fc::ChainScalars> sc(C);
+    HIP_TRY(hipMemcpy(flip_count, r->d_flip_count, C * n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(occupancy, r->d_occ_acc, C * n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(last_accept, r->d_last_accept, C * n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(a.data(), r->d_assign, a.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < C; ++c) {
+        // sum_t L(a_t) = L(a_0) s_1 + L(a_1)(s_2 - s_1) + ... = L(a_now) T - sum_flips (L_new - L_old) s
+        const int64_t T = sc[c].steps + 1;
+        for (size_t u = 0; u < n; ++u) occupancy[c * n + u] += (int64_t)r->labels[a[c * r->npad + u]] * T;
+    }
+    return FC_OK;
+}
+
+int fc_run_read_wait_expected(fc_run *r, double *out) {
+    if (!r || !out) return fail(FC_ERR_ARG, "fc_run_read_wait_expected: null argument");
+    if (!r->d_nb_hist) return fail(FC_ERR_ARG, "fc_run_read_wait_expected: FC_DIAG_HIST not enabled");
+    if (int rc = fc_run_sync(r)) return rc;
+    const size_t n = r->g.n, C = r->n_chains;
+    std::vector<int64_t> h(C * (n + 1));
+    HIP_TRY(hipMemcpy(h.data(), r->d_nb_hist, h.size() * 8, hipMemcpyDeviceToHost));
+    // geom_wait (:147-148): np.random.geometric(p) - 1 with p = |B| / (N^k - 1): mean 1/p - 1
+    const double M = std::pow((double)n, (double)r->p.k) - 1.0;
+    for (size_t c = 0; c < C; ++c) {
+        double s = 0.0;
+        for (size_t b = 1; b <= n; ++b)
+            if (h[c * (n + 1) + b]) s += (double)h[c * (n + 1) + b] * (M / (double)b - 1.0);
+        out[c] = s;
     }
     return FC_OK;
 }

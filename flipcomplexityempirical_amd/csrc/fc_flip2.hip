@@ -812,6 +812,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
                 }
             }
+            if ((p.diag & FC_DIAG_FLIPS_EXACT) && is_acc) {
+                // the corrected companions: one count per accepted
+                // flip, the label's time integral as -(L_new - L_old) t per flip (+ L_now T at
+                // read-out, fc_run_read_flips_exact), the flip's yield; commuting updates only
+                const size_t o = (size_t)c * n + v;
+                const int64_t dl = (int64_t)p.labels[1 - av] - (int64_t)p.labels[av];
+                atomicAdd((unsigned long long *)(p.flip_count + o), 1ull);
+                atomicAdd((unsigned long long *)(p.occ_acc + o), (unsigned long long)(-dl * t_acc));
+                atomicMax((unsigned long long *)(p.last_accept + o), (unsigned long long)t_acc);
+            }
             if ((p.diag & FC_DIAG_EDGES) && is_acc) {
                 // cut_times[e] (yields with e cut, :383-384) = sum of the yields at which e turns
                 // uncut - sum of those at which it turns cut (+ the yield count while it is cut:

@@ -107,6 +107,9 @@ struct KParams {
     int64_t *num_flips;         // [n_chains * n]
     int64_t *part_sum;          // [n_chains * n]
     int64_t *last_flipped;      // [n_chains * n]
+    int64_t *flip_count;        // [n_chains * n] FC_DIAG_FLIPS_EXACT: accepted flips
+    int64_t *occ_acc;           // [n_chains * n] ... -sum over flips of (L_new - L_old) * t
+    int64_t *last_accept;       // [n_chains * n] ... yield of the last accepted flip
     fc_record *trace;           // [trace_chains * trace_cap]
     int32_t trace_chains;
     int64_t trace_cap;

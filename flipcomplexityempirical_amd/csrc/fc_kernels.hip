@@ -743,7 +743,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             const uint64_t hm = __ballot(is_acc && cut_after >= p.hit_lo && cut_after <= p.hit_hi);
             if (hm) hit_time = (int64_t)__shfl((long long)t_acc, __builtin_ctzll(hm));
         }
-        if (FULL && (p.diag & (FC_DIAG_HIST | FC_DIAG_FLIPS | FC_DIAG_EDGES))) {
+        if (FULL && (p.diag & (FC_DIAG_HIST | FC_DIAG_FLIPS | FC_DIAG_FLIPS_EXACT | FC_DIAG_EDGES))) {
             if (p.diag & FC_DIAG_HIST) {
                 if (is_acc) {
                     atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
@@ -772,6 +772,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                     atomicAdd((unsigned long long *)(ps + v), (unsigned long long)(-(int64_t)p.labels[tgt] * (t_last - old)));
                     atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
                 }
+            }
+            if ((p.diag & FC_DIAG_FLIPS_EXACT) && is_acc) {
+                // corrected companions (App. A.6), as in fc_flip2.hip
+                const size_t o = (size_t)c * n + v;
+                const int64_t dl = (int64_t)p.labels[tgt] - (int64_t)p.labels[av];
+                atomicAdd((unsigned long long *)(p.flip_count + o), 1ull);
+                atomicAdd((unsigned long long *)(p.occ_acc + o), (unsigned long long)(-dl * t_acc));
+                atomicMax((unsigned long long *)(p.last_accept + o), (unsigned long long)t_acc);
             }
             if ((p.diag & FC_DIAG_EDGES) && is_acc) {
                 // cut_times[e] = sum of the yields at which e turns uncut - sum of those at which

@@ -312,6 +312,24 @@ class FlipRun:
                                             _p(lf, ctypes.c_int64)))
         return nf, ps, lf
 
+    def flips_exact(self):
+        """FC_DIAG_FLIPS_EXACT: (flip_count, occupancy, last_accept) [chains, n] -- the corrected
+        companions of :meth:`flips` (include/flipchain.h)."""
+        n = self.graph.n
+        fc_ = np.zeros((self.n_chains, n), dtype=np.int64)
+        occ = np.zeros((self.n_chains, n), dtype=np.int64)
+        la = np.zeros((self.n_chains, n), dtype=np.int64)
+        check(_lib.load().fc_run_read_flips_exact(self.handle, _p(fc_, ctypes.c_int64), _p(occ, ctypes.c_int64),
+                                                  _p(la, ctypes.c_int64)))
+        return fc_, occ, la
+
+    def wait_expected(self) -> np.ndarray:
+        """Rao-Blackwellised wait.txt companion (App. A.6 quirk 3): per chain, the sum over yields
+        of E[geom_wait | |B|] = (N^k - 1)/|B| - 1 (:147-148), from the |B| histogram."""
+        out = np.zeros(self.n_chains, dtype=np.float64)
+        check(_lib.load().fc_run_read_wait_expected(self.handle, _p(out, ctypes.c_double)))
+        return out
+
     # ---- series diagnostics (FC_DIAG_SERIES) ------------------------------------------
     def events(self, chain: int = 0) -> np.ndarray:
         """Accepted flips of ``chain`` in the current series window (``fc_event``)."""

@@ -55,6 +55,10 @@ extern "C" {
 #define FC_DIAG_SERIES 0x10u     /* per-chain log of accepted flips (fc_event): the rce / rbn
                                     series of :367-369 in run-length form; feeds
                                     fc_run_autocorr and the slope / angle series (:371-392)  */
+#define FC_DIAG_FLIPS_EXACT 0x20u /* the corrected companions of FC_DIAG_FLIPS (SURVEY App. A.6
+                                    quirks 1-2): accepted flips per node, the time integral of
+                                    each node's label over all yields, and the yield of its last
+                                    accepted flip -- fc_run_read_flips_exact                   */
 
 /* fc_params.accept: the accept callable (k = 2).  The variants are the reference's
  * alternatives, built but unused by its sweeps.                           */
@@ -266,6 +270,20 @@ int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist);      /* [c
 int fc_run_read_edges(fc_run *r, int64_t *cut_times);                     /* [c*E], finalised     */
 /* num_flips / part_sum / last_flipped [c*n], finalised as grid_chain_sec11.py:416-418. */
 int fc_run_read_flips(fc_run *r, int64_t *num_flips, int64_t *part_sum, int64_t *last_flipped);
+/* FC_DIAG_FLIPS_EXACT, [c*n] each (the statistics the driver's :396-400 / :416-418 aim at,
+ * without its quirks; App. A.6):
+ *   flip_count[u]  = accepted flips of u (the driver's num_flips counts every yield of the state
+ *                    u's flip created, because part.flips is stale on rejected steps);
+ *   occupancy[u]   = sum over all yields t of labels[a_t(u)] (the driver's part_sum drops the
+ *                    final segment of every node that flipped at least once);
+ *   last_accept[u] = yield index of u's last accepted flip (0: never flipped).
+ * FC_ERR_ARG if FC_DIAG_FLIPS_EXACT is off; ReCom runs do not keep them (FC_ERR_UNSUPPORTED at
+ * fc_run_create). */
+int fc_run_read_flips_exact(fc_run *r, int64_t *flip_count, int64_t *occupancy, int64_t *last_accept);
+/* Rao-Blackwellised companion of wait.txt (App. A.6 quirk 3: the cached geometric sample repeats
+ * on rejected steps): out[c] = sum over yields of E[geom_wait | |B|] = (N^k - 1) / |B| - 1
+ * (geom_wait :147-148), from the |B| histogram.  Needs FC_DIAG_HIST (FC_ERR_ARG otherwise). */
+int fc_run_read_wait_expected(fc_run *r, double *out);
 /* ---- series diagnostics (FC_DIAG_SERIES): the per-yield lists rce / rbn (:367-369) ----- */
 /* Events of one chain's current window (*len = events recorded, may exceed cap). */
 int fc_run_read_events(fc_run *r, int32_t chain, fc_event *out, int64_t cap, int64_t *len);

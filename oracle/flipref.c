@@ -188,6 +188,8 @@ static void yield_state(ctx_t *c, fr_stats *st, fr_outputs *o, int64_t t) {
             o->last_flipped[f] = t;
             o->num_flips[f] += 1;
         }
+        if (o->occupancy)                                   /* the label's time integral  */
+            for (int32_t u = 0; u < p->n; ++u) o->occupancy[u] += p->labels[(int)c->a[u]];
     }
 }
 
@@ -237,6 +239,7 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
     if (p->proposal == FR_PROPOSE_BI_SIGN && p->k != 2) return -2;
     if (p->proposal != FR_PROPOSE_BI_SIGN && p->proposal != FR_PROPOSE_PAIR) return -2;
     if (o && o->num_flips && (!o->part_sum || !o->last_flipped || !p->labels)) return -2;
+    if (o && o->occupancy && (!o->flip_count || !o->last_accept || !p->labels)) return -2;
     const int32_t n = p->n;
     memset(st, 0, sizeof *st);
     st->last_flip = -1;
@@ -285,6 +288,8 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
                 o->num_flips[u] = 0; o->last_flipped[u] = 0;
                 o->part_sum[u] = p->labels[(int)c.a[u]];       /* grid_chain_sec11.py:219 */
             }
+        if (o->occupancy)
+            for (int32_t u = 0; u < n; ++u) { o->flip_count[u] = 0; o->occupancy[u] = 0; o->last_accept[u] = 0; }
         o->trace_len = 0;
     }
 
@@ -396,6 +401,7 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
             st->accepted += 1;
             st->last_flip = v;
             st->wait_cur = geom_wait(p, draw, 1, c.nb);
+            if (o && o->occupancy) { o->flip_count[v] += 1; o->last_accept[v] = st->steps; }
         }
         yield_state(&c, st, o, st->steps);
         if (o && o->trace && o->trace_len < o->trace_cap) {

@@ -113,6 +113,9 @@ typedef struct fr_outputs {
     int64_t *nb_hist;                                         /* [n+1] nullable      */
     int64_t *cut_times;                                       /* [E]   nullable      */
     int64_t *num_flips, *part_sum, *last_flipped;             /* [n]   nullable      */
+    /* corrected companions, [n] nullable together:
+     * accepted flips, sum over yields of labels[a_t], yield of the last accepted flip  */
+    int64_t *flip_count, *occupancy, *last_accept;
 } fr_outputs;
 
 /* 0 ok; -1 initial state invalid (ValueError in MarkovChain.__init__); -2 bad args;

@@ -127,7 +127,10 @@ class FrOutputs(ctypes.Structure):
                 ("final_assign", _P(ctypes.c_int8)), ("cut_hist", _P(ctypes.c_int64)),
                 ("nb_hist", _P(ctypes.c_int64)), ("cut_times", _P(ctypes.c_int64)),
                 ("num_flips", _P(ctypes.c_int64)), ("part_sum", _P(ctypes.c_int64)),
-                ("last_flipped", _P(ctypes.c_int64))]
+                ("last_flipped", _P(ctypes.c_int64)),
+                # corrected companions, flipref.h fr_outputs
+                ("flip_count", _P(ctypes.c_int64)), ("occupancy", _P(ctypes.c_int64)),
+                ("last_accept", _P(ctypes.c_int64))]
 
 
 def build_lib(force: bool = False) -> str:
@@ -185,7 +188,7 @@ class CRef:
             want_edges: bool = False, want_flips: bool = False, proposal: int = 0, wmax: int = 0,
             accept: int = 0, con_valid: int = 0, con_accept: int = 0, beta: float = 0.0,
             boundary: Optional[np.ndarray] = None, pinned: Optional[np.ndarray] = None,
-            wait0_words: Optional[np.ndarray] = None) -> Dict:
+            wait0_words: Optional[np.ndarray] = None, want_exact_flips: bool = False) -> Dict:
         n, E = spec.n, spec.n_edges
         row_ptr = np.ascontiguousarray(spec.row_ptr, dtype=np.int32)
         col_idx = np.ascontiguousarray(spec.col_idx, dtype=np.int32)
@@ -217,11 +220,15 @@ class CRef:
         nf = np.zeros(n, dtype=np.int64) if want_flips else None
         ps = np.zeros(n, dtype=np.int64) if want_flips else None
         lf = np.zeros(n, dtype=np.int64) if want_flips else None
+        xfc, xocc, xla = ((np.zeros(n, dtype=np.int64) for _ in range(3)) if want_exact_flips
+                          else (None, None, None))
         o = FrOutputs(trace=ctypes.cast(trace.ctypes.data, _P(FrRecord)) if trace is not None else _P(FrRecord)(),
                       trace_cap=trace_cap, trace_len=0, final_assign=_ptr(final, ctypes.c_int8),
                       cut_hist=_ptr(cut_hist, ctypes.c_int64), nb_hist=_ptr(nb_hist, ctypes.c_int64),
                       cut_times=_ptr(cut_times, ctypes.c_int64), num_flips=_ptr(nf, ctypes.c_int64),
-                      part_sum=_ptr(ps, ctypes.c_int64), last_flipped=_ptr(lf, ctypes.c_int64))
+                      part_sum=_ptr(ps, ctypes.c_int64), last_flipped=_ptr(lf, ctypes.c_int64),
+                      flip_count=_ptr(xfc, ctypes.c_int64), occupancy=_ptr(xocc, ctypes.c_int64),
+                      last_accept=_ptr(xla, ctypes.c_int64))
         st = FrStats()
         rc = self.lib.fr_run(ctypes.byref(p), _ptr(init, ctypes.c_int8), ctypes.byref(st), ctypes.byref(o))
         if rc == -1:
@@ -237,6 +244,8 @@ class CRef:
             out["cut_times"] = cut_times
         if want_flips:
             out["num_flips"], out["part_sum"], out["last_flipped"] = nf, ps, lf
+        if want_exact_flips:
+            out["flip_count"], out["occupancy"], out["last_accept"] = xfc, xocc, xla
         return out
 
 
