@@ -481,14 +481,20 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     }
                     FC_STAMP(t_mk);
                     FC_PROF(18, t_mk - t_it1);
-                    // alpha (later slots), entering non-hits and beta (later candidates)
-                    bool conf = has && ms < lane;
+                    // alpha (later slots), entering non-hits and beta (later candidates); every
+                    // lane reads (cells are valid nodes on idle lanes too), so the reads issue
+                    // back to back instead of one exec-masked round trip each
+                    int smk[RMAX];
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i) smk[i] = smark[cell[i]];
+                    bool conf = ms < lane;
 #pragma unroll
                     for (int i = 0; i < RMAX; ++i) {
                         const bool nb_i = (nbr >> i) & 1u;
-                        conf |= has && (int)smark[cell[i]] < lane;
-                        conf |= inK && nb_i && mn[i] < lane;
+                        conf |= smk[i] < lane;
+                        conf |= inK & nb_i & (mn[i] < lane);
                     }
+                    conf &= has;
                     const uint64_t XX = __ballot(conf && lane > pos && lane < end);
                     if (XX) {
                         x = __builtin_ctzll(XX);
@@ -498,10 +504,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     // non-hit draws whose node a committed flip pulls into the boundary would
                     // now be proposals: the batch ends before the first of them
                     int t = trunc_off;
+                    int mk[NSUB], so[NSUB];
+#pragma unroll
+                    for (int r = 0; r < NSUB; ++r) mk[r] = nmark[rv[r] < 0 ? 0 : rv[r]];
+#pragma unroll
+                    for (int r = 0; r < NSUB; ++r) so[r] = (int)slot[192 + (mk[r] & 63)];
 #pragma unroll
                     for (int r = 0; r < NSUB; ++r) {
-                        const int mk = nmark[rv[r] < 0 ? 0 : rv[r]];
-                        const bool tr = rv[r] >= 0 && mk < x && 64 * r + lane > (int)slot[192 + (mk & 63)];
+                        const bool tr = (rv[r] >= 0) & (mk[r] < x) & (64 * r + lane > so[r]);
                         const uint64_t TR = __ballot(tr);
                         if (TR) t = min(t, 64 * r + __builtin_ctzll(TR));
                     }
@@ -644,9 +654,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             if (ent) {
                 const int off_f = rl32(off_l, f);
                 int t_na = trunc_off;
+                int fr[NSUB];
+#pragma unroll
+                for (int r = 0; r < NSUB; ++r) fr[r] = fcnt[rv[r] < 0 ? 0 : rv[r]];
 #pragma unroll
                 for (int r = 0; r < NSUB; ++r) {
-                    const bool tr = (rv[r] >= 0) & (64 * r + lane > off_f) && fcnt[rv[r] < 0 ? 0 : rv[r]] != 0;
+                    const bool tr = (rv[r] >= 0) & (64 * r + lane > off_f) & (fr[r] != 0);
                     const uint64_t m2 = __ballot(tr);
                     if (m2) t_na = min(t_na, 64 * r + __builtin_ctzll(m2));
                 }
