@@ -65,6 +65,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     // creating draw, |B| after the flip, yields so far); see wait_flush below
     uint64_t *q_d = (uint64_t *)(nmark + npad + 16);
     uint32_t *q_nb = (uint32_t *)(q_d + kWaitQ), *q_run = q_nb + kWaitQ;
+    uint64_t *misc = (uint64_t *)(q_run + kWaitQ);  // [2]: launch start time (read back, not held)
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
     // ---- load the chain into LDS -------------------------------------------------------
@@ -81,7 +82,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     ChainScalars *scp = p.sc + c;
     uint64_t draw = scp->draw;
     int64_t steps = scp->steps;  // index of the current yield
-    int64_t bfs_calls = scp->bfs_calls, bfs_levels = scp->bfs_levels;
     int64_t trace_len = FULL ? scp->trace_len : 0;
     int64_t ev_len = FULL ? scp->ev_len : 0, hit_time = FULL ? scp->hit_time : 0;
     int cut = scp->cut, nb = scp->nb;
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
 
     // per-lane accumulators, reduced once per launch
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
-    uint32_t n_prop = 0, n_acc = 0, n_ic = 0, n_ip = 0;
+    int64_t n_prop = 0, n_acc = 0, n_ic = 0, n_ip = 0;  // wave-uniform (scalar) counters
 #ifdef FC_PHASE_PROF
     int64_t *prof_acc = (int64_t *)(base + p.chain_lds_bytes - kProfSlots * 8);
     if (lane < kProfSlots) prof_acc[lane] = 0;
@@ -145,21 +145,28 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         qn = 0;
         compiler_fence();
     };
-    int prio = 0;
-    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    const float eta = p.eta ? (float)p.eta[p.eta_parity ^ 1] * (float)p.n_steps * (1.0f / 1024.0f) : 0.0f;
+    int prio = 0;  // bits 0-1: the issue priority set; bits 2-3: batches since it was last chosen
+    if (lane == 0) {
+        misc[0] = __builtin_amdgcn_s_memrealtime();
+        // the previous launch's slowest-chain pace, scaled to this launch (0: none yet)
+        const float eta0 = p.eta ? (float)p.eta[p.eta_parity ^ 1] * (float)p.n_steps * (1.0f / 1024.0f) : 0.0f;
+        misc[1] = (uint64_t)__float_as_uint(eta0);
+    }
+    compiler_fence();
     while (rem > 0) {
-        if (p.prio_nb[0] > 0) {
+        // re-chosen every fourth batch (it moves slowly; scheduling only)
+        if (p.prio_nb[0] > 0 && ((prio += 4) & 12) == 0) {
             const int done = (int)p.n_steps - rem;
+            const float eta = __uint_as_float((uint32_t)misc[1]);
             int lv;
             if (eta > 0.0f && done * 16 >= (int)p.n_steps) {
-                const float pr = (float)(__builtin_amdgcn_s_memrealtime() - rt0) * (float)p.n_steps / ((float)done * eta);
+                const float pr = (float)(__builtin_amdgcn_s_memrealtime() - misc[0]) * (float)p.n_steps / ((float)done * eta);
                 lv = (pr > p.prio_th[0]) + (pr > p.prio_th[1]) + (pr > p.prio_th[2]);
             } else {
                 lv = (nb < p.prio_nb[0]) + (nb < p.prio_nb[1]) + (nb < p.prio_nb[2]);
             }
-            if (lv != prio) {
-                prio = lv;
+            if (lv != (prio & 3)) {
+                prio = (prio & ~3) | lv;
                 switch (lv) {
                     case 0: __builtin_amdgcn_s_setprio(0); break;
                     case 1: __builtin_amdgcn_s_setprio(1); break;
@@ -178,7 +185,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // ---- 1. draws -> nodes; boundary hits packed, in draw order, into <= 64 slots ----
         int nh = 0;   // boundary hits seen
         int gen = 0;  // draws generated (offsets 0..gen-1 of this batch)
-        int rv[NSUB]; // node of this lane's non-hit draw in round r (offset 64 r + lane), -1: none
+        // this lane's non-hit draw in round r (offset 64 r + lane): node | (slots drawn before it
+        // << 16), -1: none.  "slot s precedes the draw" is then s < rv >> 16.
+        int rv[NSUB];
 #pragma unroll
         for (int r = 0; r < NSUB; ++r) {
             rv[r] = -1;
@@ -222,7 +231,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             } else {
                 gen = (uint64_t)(gen + 64) < room ? gen + 64 : (int)room;
             }
-            if (okd && !hitd && lane < used) rv[r] = vd;
+            if (okd && !hitd && lane < used) rv[r] = vd | (sp << 16);
             nh += cnt;
         }
         const int ns = nh < 64 ? nh : 64;
@@ -346,8 +355,15 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 if (start < 0 && ((nbrAf >> (2 * k2 + 1)) & 1u)) start = (int)(wrd >> 16);
             }
             if (!(lane < RMAX && ((nbrAf >> lane) & 1u))) my_target = -1;
-            ++bfs_calls;
-            return wave_bfs_single<RMAX>(G, a, bs, lane, rl32(v, f), rl32(av, f), my_target, start, bfs_levels);
+            // the (rare) search counts go straight to the chain's record: as loop-carried values
+            // they cost the hot loop two 64-bit registers
+            int64_t lv = 0;
+            const bool res = wave_bfs_single<RMAX>(G, a, bs, lane, rl32(v, f), rl32(av, f), my_target, start, lv);
+            if (lane == 0) {
+                atomicAdd((unsigned long long *)&scp->bfs_calls, 1ull);
+                atomicAdd((unsigned long long *)&scp->bfs_levels, (unsigned long long)lv);
+            }
+            return res;
         };
 
         while (pos < end) {
@@ -456,37 +472,41 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 if (K) {
                     const bool inK = (K >> lane) & 1ull;
                     if (inK) st |= LF_WROTE;
-                    // marks: smark[node] / nmark[neighbour] = lowest candidate lane (0xff: none)
+                    // marks: smark[node] / nmark[neighbour] = lowest candidate lane (0xff: none).
+                    // Every segment pass clears its marks (below), so the first round writes without
+                    // reading.  Stores to one byte from later instructions win (a node is a
+                    // neighbour of two candidates at different ring positions), so a lane that finds
+                    // a higher lane in one of its marks writes again.  Each round also reads what the
+                    // checks below need (the last round's values are the final ones): alpha (later
+                    // slots), beta (later candidates), entering non-hits.  Every lane reads (cells
+                    // are valid nodes on idle lanes too), so the reads issue back to back.
                     bool need = inK;
-                    int ms, mn[RMAX];
-                    for (;;) {
-                        ms = smark[v];
+                    int ms = 0xff, mn[RMAX], smk[RMAX], mk[NSUB];
 #pragma unroll
-                        for (int i = 0; i < RMAX; ++i) mn[i] = nmark[cell[i]];
-                        compiler_fence();
+                    for (int i = 0; i < RMAX; ++i) mn[i] = 0xff;
+                    for (;;) {
+                        FC_PROF(21, 1);
                         *((need && ms > lane) ? &smark[v] : dum) = (uint8_t)lane;
 #pragma unroll
                         for (int i = 0; i < RMAX; ++i)
                             *((need && ((nbr >> i) & 1u) && mn[i] > lane) ? &nmark[cell[i]] : dum) = (uint8_t)lane;
                         compiler_fence();
                         ms = smark[v];
-                        bool again = ms > lane;
 #pragma unroll
                         for (int i = 0; i < RMAX; ++i) {
                             mn[i] = nmark[cell[i]];
-                            again |= ((nbr >> i) & 1u) && mn[i] > lane;
+                            smk[i] = smark[cell[i]];
                         }
+#pragma unroll
+                        for (int r = 0; r < NSUB; ++r) mk[r] = nmark[rv[r] < 0 ? 0 : (rv[r] & 0xffff)];
+                        bool again = ms > lane;
+#pragma unroll
+                        for (int i = 0; i < RMAX; ++i) again |= ((nbr >> i) & 1u) && mn[i] > lane;
                         need = need && again;
                         if (!__any(need)) break;
                     }
                     FC_STAMP(t_mk);
                     FC_PROF(18, t_mk - t_it1);
-                    // alpha (later slots), entering non-hits and beta (later candidates); every
-                    // lane reads (cells are valid nodes on idle lanes too), so the reads issue
-                    // back to back instead of one exec-masked round trip each
-                    int smk[RMAX];
-#pragma unroll
-                    for (int i = 0; i < RMAX; ++i) smk[i] = smark[cell[i]];
                     bool conf = ms < lane;
 #pragma unroll
                     for (int i = 0; i < RMAX; ++i) {
@@ -501,17 +521,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         stale_seg = true;
                         FC_PROF(13, 1);
                     }
-                    // non-hit draws whose node a committed flip pulls into the boundary would
-                    // now be proposals: the batch ends before the first of them
+                    // non-hit draws whose node a committed flip (a candidate before the draw)
+                    // pulls into the boundary would now be proposals: the batch ends before the
+                    // first of them
                     int t = trunc_off;
-                    int mk[NSUB], so[NSUB];
-#pragma unroll
-                    for (int r = 0; r < NSUB; ++r) mk[r] = nmark[rv[r] < 0 ? 0 : rv[r]];
-#pragma unroll
-                    for (int r = 0; r < NSUB; ++r) so[r] = (int)slot[192 + (mk[r] & 63)];
 #pragma unroll
                     for (int r = 0; r < NSUB; ++r) {
-                        const bool tr = (rv[r] >= 0) & (mk[r] < x) & (64 * r + lane > so[r]);
+                        const bool tr = (rv[r] >= 0) & (mk[r] < x) & (mk[r] < (rv[r] >> 16));
                         const uint64_t TR = __ballot(tr);
                         if (TR) t = min(t, 64 * r + __builtin_ctzll(TR));
                     }
@@ -566,6 +582,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     ng1 -= dG;
                     last_flip = rl32(v, L);
                     compiler_fence();
+                }
+                if (st & LF_WROTE) {  // clear this pass's marks: the next pass starts clean
+                    smark[v] = 0xff;
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i) *(((nbr >> i) & 1u) ? &nmark[cell[i]] : dum) = 0xff;
+                    st &= ~LF_WROTE;
                 }
                 FC_STAMP(t_sg1);
                 FC_PROF(11, t_sg1 - t_it1);
@@ -652,14 +674,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             // (the counts written above are read back: a non-hit node had no foreign neighbour
             // when it was drawn, and a flip before f that gave it one has cut the batch already)
             if (ent) {
-                const int off_f = rl32(off_l, f);
                 int t_na = trunc_off;
                 int fr[NSUB];
 #pragma unroll
-                for (int r = 0; r < NSUB; ++r) fr[r] = fcnt[rv[r] < 0 ? 0 : rv[r]];
+                for (int r = 0; r < NSUB; ++r) fr[r] = fcnt[rv[r] < 0 ? 0 : (rv[r] & 0xffff)];
 #pragma unroll
                 for (int r = 0; r < NSUB; ++r) {
-                    const bool tr = (rv[r] >= 0) & (64 * r + lane > off_f) & (fr[r] != 0);
+                    const bool tr = (rv[r] >= 0) & ((rv[r] >> 16) > f) & (fr[r] != 0);
                     const uint64_t m2 = __ballot(tr);
                     if (m2) t_na = min(t_na, 64 * r + __builtin_ctzll(m2));
                 }
@@ -717,15 +738,17 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         const bool done = lane < end;
         const bool is_acc = (st & ST_AC) != 0;
         const bool proposed = (st & LF_HIT) && done;
-        n_prop += proposed ? 1u : 0u;
-        n_acc += is_acc ? 1u : 0u;
-        n_ic += (st & ST_IC) ? 1u : 0u;
-        n_ip += (st & ST_IP) ? 1u : 0u;
+        n_prop += __popcll(__ballot(proposed));
+        n_acc += __popcll(__ballot(is_acc));
+        n_ic += __popcll(__ballot((st & ST_IC) != 0));
+        n_ip += __popcll(__ballot((st & ST_IP) != 0));
         const uint64_t ACCM = __ballot(is_acc);
         const uint64_t VSM = __ballot((st & ST_VS) != 0);
-        const uint64_t later_acc = ACCM & ~bits_below(lane + 1);
+        int ln = lane;  // opaque copy: lane masks derived from it are recomputed, not hoisted and spilled
+        asm volatile("" : "+v"(ln));
+        const uint64_t later_acc = ACCM & ~bits_below(ln + 1);
         const int next_acc = later_acc ? __builtin_ctzll(later_acc) : end;
-        const int run_len = is_acc ? 1 + __popcll(VSM & lane_range(lane + 1, next_acc)) : 0;
+        const int run_len = is_acc ? 1 + __popcll(VSM & lane_range(ln + 1, next_acc)) : 0;
         const int first_acc = ACCM ? __builtin_ctzll(ACCM) : end;
         const int r0 = __popcll(VSM & bits_below(first_acc));
         int64_t my_wait = 0;
@@ -769,9 +792,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             }
         }
         if constexpr (FULL) {
-            const int64_t t_acc = steps0 + __popcll(VSM & bits_below(lane + 1));  // yield index of this lane
+            const int64_t t_acc = steps0 + __popcll(VSM & bits_below(ln + 1));  // yield index of this lane
             if ((p.diag & FC_DIAG_SERIES) && ACCM) {
-                const int64_t idx = ev_len + __popcll(ACCM & bits_below(lane));
+                const int64_t idx = ev_len + __popcll(ACCM & bits_below(ln));
                 if (is_acc && idx < p.ev_cap) {
                     fc_event ev;
                     ev.t = t_acc;
@@ -852,11 +875,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             }
             if (trace_on) {
                 const uint64_t PM = __ballot(proposed);
-                const uint64_t mine = ACCM & bits_below(lane + 1);
+                const uint64_t mine = ACCM & bits_below(ln + 1);
                 const int src = mine ? 63 - __builtin_clzll(mine) : 0;
                 const int c_j = __shfl(cut_after, src), n_j = __shfl(nb_after, src);
                 const long long w_j = __shfl((long long)my_wait, src);
-                const int64_t idx = trace_len + __popcll(PM & bits_below(lane));
+                const int64_t idx = trace_len + __popcll(PM & bits_below(ln));
                 if (proposed && idx < p.trace_cap) {
                     fc_record &rr = p.trace[(size_t)c * p.trace_cap + idx];
                     const bool valid = (st & ST_VS) != 0;
@@ -892,14 +915,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
 #ifdef FC_EXP_DEAL_TIME
-    if (p.ctime && lane == 0) p.ctime[c] = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - rt0, (uint64_t)0xffffffffu);
+    if (p.ctime && lane == 0) p.ctime[c] = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - misc[0], (uint64_t)0xffffffffu);
 #else
     // the chain's own work this launch (draws: a short boundary costs many per step), not its
     // duration, which its SIMD-mates stretch
     if (p.ctime && lane == 0) p.ctime[c] = (uint32_t)min(draw - scp->draw, (uint64_t)0xffffffffu);
 #endif
     if (p.eta && rem == 0 && lane == 0) {  // this launch's pace, for the next one's priorities
-        const uint64_t el = __builtin_amdgcn_s_memrealtime() - rt0;
+        const uint64_t el = __builtin_amdgcn_s_memrealtime() - misc[0];
         atomicMax(&p.eta[p.eta_parity], (uint32_t)min(el * 1024ull / (uint64_t)max((int)p.n_steps, 1), 0xffffffffull));
     }
 #ifdef FC_PHASE_PROF
@@ -917,7 +940,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             gf[i] = ((const uint4 *)fcnt)[i];
         }
     }
-    int64_t cnt_prop = n_prop, cnt_acc = n_acc, cnt_ic = n_ic, cnt_ip = n_ip;
+    const int64_t cnt_prop = n_prop, cnt_acc = n_acc, cnt_ic = n_ic, cnt_ip = n_ip;  // already wave totals
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         acc_cut += __shfl_xor((long long)acc_cut, off);
@@ -925,10 +948,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         acc_wait += __shfl_xor((long long)acc_wait, off);
         acc_cut2 += __shfl_xor((long long)acc_cut2, off);
         acc_nb2 += __shfl_xor((long long)acc_nb2, off);
-        cnt_prop += __shfl_xor((long long)cnt_prop, off);
-        cnt_acc += __shfl_xor((long long)cnt_acc, off);
-        cnt_ic += __shfl_xor((long long)cnt_ic, off);
-        cnt_ip += __shfl_xor((long long)cnt_ip, off);
     }
     if (lane == 0) {
         scp->draw = draw;
@@ -937,8 +956,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         scp->accepted += cnt_acc;
         scp->inv_contig += cnt_ic;
         scp->inv_pop += cnt_ip;
-        scp->bfs_calls = bfs_calls;
-        scp->bfs_levels = bfs_levels;
         if (FULL) {
             scp->trace_len = trace_len;
             scp->ev_len = ev_len;

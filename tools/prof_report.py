@@ -31,9 +31,9 @@ if S >= 16:
         b = max(x[5], 1)
         print(f"{g:3d} | {x[13]/b:6.3f} {x[14]/b:6.3f} {x[15]/b:6.3f}")
 if S >= 24:
-    print("grp | reeval: cycles per call, calls per batch | segment: marks, marks+conflicts+entering per segment")
+    print("grp | reeval: cycles per call, calls per batch | segment: marks, marks+conflicts+entering per segment, mark rounds")
     for g in range(G):
         x = last[np.arange(C) % G == g].mean(axis=0)
         b = max(x[5], 1)
-        print(f"{g:3d} | {x[16]/max(x[17],1):8.0f} {x[17]/b:6.2f} | {x[18]/max(x[12],1):8.0f} {x[19]/max(x[12],1):8.0f}")
+        print(f"{g:3d} | {x[16]/max(x[17],1):8.0f} {x[17]/b:6.2f} | {x[18]/max(x[12],1):8.0f} {x[19]/max(x[12],1):8.0f} {x[21]/max(x[12],1):6.2f}")
 print("max chain total Mcyc", last[:, 0].max() / 1e6, "argmax", int(last[:, 0].argmax()))
