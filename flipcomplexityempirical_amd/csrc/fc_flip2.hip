@@ -306,7 +306,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // on.  A slot whose node left the boundary is then a non-proposal draw, as it is in
         // the one-draw-at-a-time chain.  The commit marks of the segment passes so far are
         // cleared first: every slot's view is current again.
-        auto reeval = [&](int from) {
+        // vfx >= 0 (one event at a time): node vfx is the only one flipped since the slots' last
+        // evaluation, and eqx marks it in this lane's ring, so the view is updated in registers
+        // (no ring reads; the threshold read issues beside the slot reads)
+        auto reeval = [&](int from, int vfx, uint32_t eqx) {
             FC_STAMP(t_re0);
             if (st & LF_WROTE) {
                 smark[v] = 0xff;
@@ -317,23 +320,35 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             compiler_fence();
             if (has && lane >= from) {
                 const uint32_t lkl = slot[256 + lane];
-                const uint32_t lnk = lkl & 0xffffu, L2 = lkl >> 16;
-                const uint32_t fl = (1u << L2) - 1u;
-                av = a[v];
-                uint32_t ia = 0;
+                const uint32_t w1r = slot[64 + lane], w2r = slot[128 + lane];
+                if (vfx < 0) {
+                    av = a[v];
+                    uint32_t ia = 0;
 #pragma unroll
-                for (int i = 0; i < RMAX; ++i) ia |= (uint32_t)(a[cell[i]] == av) << i;
-                inA = ia & fl;
+                    for (int i = 0; i < RMAX; ++i) ia |= (uint32_t)(a[cell[i]] == av) << i;
+                    inA = ia;
+                } else {
+                    if (v == vfx) {  // its own node flipped: every ring relation inverts
+                        av = 1 - av;
+                        inA = ~inA;
+                    }
+                    inA ^= eqx;
+                }
+                // nbr has no bits at or above the ring length: these need no length mask
                 const uint32_t nbA = inA & nbr;
                 tmask = nbr & ~inA;
                 nA = __popc(nbA);
                 delta = nA - __popc(tmask);
+                const uint64_t th = T[delta + RMAX];
+                const uint32_t lnk = lkl & 0xffffu, L2 = lkl >> 16;
+                const uint32_t fl = (1u << L2) - 1u;
+                inA &= fl;
                 const uint32_t rot = L2 ? (((inA >> 1) | (inA << (L2 - 1))) & fl) : 0u;
                 const uint32_t lk = inA & rot & lnk;
                 const bool sl = one_run(nbA, fl & ~lk, fl);
                 const uint32_t vlink = (L2 >= 2 && (inA & 1u) && ((inA >> (L2 - 1)) & 1u)) ? (1u << (L2 - 1)) : 0u;
                 const bool sc = one_run(nbA, fl & ~(lk | vlink), fl);
-                const bool ac = mant53(slot[64 + lane], slot[128 + lane]) < T[delta + RMAX];
+                const bool ac = mant53(w1r, w2r) < th;
                 st = (st & (LF_EXACT | LF_GAM | LF_HAS | LF_FRZ)) | (tmask != 0u ? LF_HIT : 0u) | (ac ? LF_ACC : 0u) |
                      (sl ? LF_SLIN : 0u) | (sc ? LF_SCYC : 0u);
             }
@@ -599,7 +614,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 }
                 if (pos >= end) break;
                 if (stale_seg && AP) {  // a committed flip changed the view of a later slot
-                    reeval(pos);
+                    reeval(pos, -1, 0u);
                     continue;
                 }
                 if (u == pos) {
@@ -721,7 +736,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 target_hit = true;
                 break;
             }
-            if (aff && pos < end) reeval(pos);
+            if (aff && pos < end) reeval(pos, vf, eqm);
         }
         if (st & LF_WROTE) {  // clear this lane's marks for the next batch
             smark[v] = 0xff;
