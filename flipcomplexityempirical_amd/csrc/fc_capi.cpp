@@ -298,8 +298,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     if (recom)   // fc_recom.hip: best / spop, tree slots, component / levels, order, parent, a
         r->chain_lds_bytes = fc::recom_lds_bytes(n);
     else if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, 3 BFS bitmaps, slots, commit marks (2 npad + 16),
-                      // wait queue (16 B per entry), launch start time (16)
-        r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16 + fc::kWaitQ * 16 + 16;
+                      // wait / tally queue (24 B per entry), launch start time, pace, first queued yield (24)
+                      // (sec11: 10,016 B, so 16 chains still fill a CU's 160 KB)
+        r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16 + fc::kWaitQ * 24 + 24;
     // k > 2: with every node's ring exact (all bounded faces triangles / quadrilaterals, so the
     // rings list every face-adjacent cell) contiguity is decided by the district-graph rule
     // (fc_kernels.hip district_rule) instead of the device search, whose scratch is then not

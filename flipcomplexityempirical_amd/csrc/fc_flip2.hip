@@ -65,7 +65,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     // creating draw, |B| after the flip, yields so far); see wait_flush below
     uint64_t *q_d = (uint64_t *)(nmark + npad + 16);
     uint32_t *q_nb = (uint32_t *)(q_d + kWaitQ), *q_run = q_nb + kWaitQ;
-    uint64_t *misc = (uint64_t *)(q_run + kWaitQ);  // [2]: launch start time (read back, not held)
+    // FULL: the per-flip tallies of a queued state, applied by the same pass (tally_flush):
+    // node | old-district neighbours (ring bits) << 16, |cut| | target district << 31
+    uint32_t *q_v = q_run + kWaitQ, *q_c = q_v + kWaitQ;
+    // [3]: launch start time, previous launch's pace (read back, not held), yield of the first
+    // queued state
+    uint64_t *misc = (uint64_t *)(q_c + kWaitQ);
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
     // ---- load the chain into LDS -------------------------------------------------------
@@ -131,8 +136,79 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     // pass when it would overflow and at the end of the launch; the current state's wait is then
     // known (wait_cur) and the yields it still lasts are charged to it directly.  The sums are
     // the per-batch ones, term by term.
+    // FULL: the per-yield tallies of the queued states (grid_chain_sec11.py:367-400), in the
+    // same pass.  Issued per batch they were global atomics in every chain's serial path, and
+    // the next batch's first vector-memory wait (vmcnt counts them) waited for all of them; here
+    // the loads go first and the atomics follow back to back, once per queue.  Each entry holds
+    // its whole run: the batches that continue the queued current state add to its run length
+    // instead of issuing their own updates.  Every update commutes (sums and maxima), so the
+    // order differs from the per-batch one and the results do not.
+    auto tally_flush = [&]() {
+        if constexpr (FULL) {
+            const bool in = lane < qn;
+            const int run = in ? (int)q_run[lane] : 0;  // a launch's runs sum below 2^31
+            const int64_t t = (int64_t)misc[2] + (int64_t)(wave_scan_incl(run) - run);  // yield of the flip
+            const uint32_t qv = in ? q_v[lane] : 0u, qc = in ? q_c[lane] : 0u;
+            const int nbq = in ? (int)q_nb[lane] : 0;
+            const int u = (int)(qv & 0xffffu), cq = (int)(qc & 0x7fffffffu), tg = (int)(qc >> 31);
+            const uint32_t up = qv >> 16;  // neighbours in the old district: their edges turn cut
+            const int64_t lab_t = (int64_t)p.labels[tg], lab_o = (int64_t)p.labels[1 - tg];
+            int eid[RMAX];
+            if (in && (p.diag & FC_DIAG_EDGES)) {
+                const int4 *er = (const int4 *)(p.ring_eid + (size_t)u * RMAX);
+#pragma unroll
+                for (int j = 0; j < RMAX / 4; ++j) {
+                    const int4 e4 = er[j];
+                    eid[4 * j] = e4.x;
+                    eid[4 * j + 1] = e4.y;
+                    eid[4 * j + 2] = e4.z;
+                    eid[4 * j + 3] = e4.w;
+                }
+            }
+            if (in) {
+                if (p.diag & FC_DIAG_SERIES) {
+                    const int64_t idx = ev_len + lane;
+                    if (idx < p.ev_cap) {
+                        fc_event ev;
+                        ev.t = t;
+                        ev.v = (uint16_t)u;
+                        ev.cut = (uint16_t)cq;
+                        ev.nb = (uint16_t)nbq;
+                        ev.target = (uint8_t)tg;
+                        ev.reserved = 0;
+                        p.events[(size_t)c * p.ev_cap + idx] = ev;
+                    }
+                }
+                if (p.diag & FC_DIAG_HIST) {
+                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cq], (unsigned long long)run);
+                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nbq], (unsigned long long)run);
+                }
+                if (p.diag & FC_DIAG_FLIPS) {  // the run's share, as in the per-batch form below
+                    const size_t o = (size_t)c * n + u;
+                    const int64_t t_last = t + run - 1;
+                    atomicMax((unsigned long long *)(p.last_flipped + o), (unsigned long long)t_last);
+                    atomicAdd((unsigned long long *)(p.part_sum + o), (unsigned long long)((lab_o - lab_t) * t_last));
+                    atomicAdd((unsigned long long *)(p.num_flips + o), (unsigned long long)run);
+                }
+                if (p.diag & FC_DIAG_FLIPS_EXACT) {
+                    const size_t o = (size_t)c * n + u;
+                    atomicAdd((unsigned long long *)(p.flip_count + o), 1ull);
+                    atomicAdd((unsigned long long *)(p.occ_acc + o), (unsigned long long)(-(lab_t - lab_o) * t));
+                    atomicMax((unsigned long long *)(p.last_accept + o), (unsigned long long)t);
+                }
+                if (p.diag & FC_DIAG_EDGES) {
+                    int64_t *ea = p.edge_acc + (size_t)c * p.n_edges;
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i)
+                        if (eid[i] >= 0) atomicAdd((unsigned long long *)(ea + eid[i]), (unsigned long long)(((up >> i) & 1u) ? -t : t));
+                }
+            }
+            if (p.diag & FC_DIAG_SERIES) ev_len += qn;
+        }
+    };
     auto wait_flush = [&]() {
         compiler_fence();
+        tally_flush();
         int64_t w = 0;
         if (lane < qn) {
             const uint64_t dq = q_d[lane];
@@ -791,6 +867,24 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             acc_nb2 += (int64_t)nb0 * nb0 * r0;
             if (!defer || qn == 0) acc_wait += wait_cur * r0;  // else: the queued current state's run
         }
+        const int64_t t_acc = FULL ? steps0 + __popcll(VSM & bits_below(ln + 1)) : 0;  // yield index of this lane
+        if constexpr (FULL) {
+            // the run of the batch's start state goes on: a queued state takes it into its run
+            // (below), else it is tallied here
+            if (lane == 0 && r0 && (!defer || qn == 0)) {
+                if (p.diag & FC_DIAG_HIST) {
+                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut0], (unsigned long long)r0);
+                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb0], (unsigned long long)r0);
+                }
+                if ((p.diag & FC_DIAG_FLIPS) && last_flip0 >= 0) {
+                    const int64_t lsum = (int64_t)p.labels[0] + (int64_t)p.labels[1];
+                    const size_t o = (size_t)c * n + last_flip0;
+                    atomicMax((unsigned long long *)(p.last_flipped + o), (unsigned long long)(steps0 + r0));
+                    atomicAdd((unsigned long long *)(p.part_sum + o), (unsigned long long)((lsum - 2 * (int64_t)p.labels[a_last0]) * r0));
+                    atomicAdd((unsigned long long *)(p.num_flips + o), (unsigned long long)r0);
+                }
+            }
+        }
         if (defer) {
             if (lane == 0 && r0 && qn > 0) q_run[qn - 1] += (uint32_t)r0;
             const int na = __popcll(ACCM);
@@ -801,14 +895,18 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     q_d[qi] = d;
                     q_nb[qi] = (uint32_t)nb_after;
                     q_run[qi] = (uint32_t)run_len;
+                    if constexpr (FULL) {
+                        q_v[qi] = (uint32_t)v | ((inA & nbr) << 16);
+                        q_c[qi] = (uint32_t)cut_after | ((uint32_t)(1 - av) << 31);
+                        if (qi == 0) misc[2] = (uint64_t)t_acc;
+                    }
                 }
                 qn += na;
                 compiler_fence();
             }
         }
         if constexpr (FULL) {
-            const int64_t t_acc = steps0 + __popcll(VSM & bits_below(ln + 1));  // yield index of this lane
-            if ((p.diag & FC_DIAG_SERIES) && ACCM) {
+            if (!defer && (p.diag & FC_DIAG_SERIES) && ACCM) {
                 const int64_t idx = ev_len + __popcll(ACCM & bits_below(ln));
                 if (is_acc && idx < p.ev_cap) {
                     fc_event ev;
@@ -829,17 +927,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     hit_time = steps0 + __popcll(VSM & bits_below(hl + 1));
                 }
             }
-            if (p.diag & FC_DIAG_HIST) {
-                if (is_acc) {
-                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
-                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb_after], (unsigned long long)run_len);
-                }
-                if (lane == 0 && r0) {
-                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut0], (unsigned long long)r0);
-                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb0], (unsigned long long)r0);
-                }
+            // per batch only when the queue is off (trace, tape): else tally_flush
+            if (!defer && (p.diag & FC_DIAG_HIST) && is_acc) {
+                atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
+                atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb_after], (unsigned long long)run_len);
             }
-            if (p.diag & FC_DIAG_FLIPS) {
+            if (!defer && (p.diag & FC_DIAG_FLIPS) && is_acc) {
                 // part.flips is stale on rejected steps: every yield of a run repeats the update
                 // part_sum[f] -= a[f] * (t - last_flipped[f]) for the node f whose flip created
                 // the state (grid_chain_sec11.py:396-400).  With two districts a node's label
@@ -848,22 +941,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 // run adds (L0 + L1 - 2 a_r) per yield it lasts, and the read-out replaces the
                 // last run's share (fc_run_read_flips).  Only commuting adds and a max remain,
                 // so flips of one batch may share nodes.
+                // (the start state's run: above)
                 int64_t *nf = p.num_flips + (size_t)c * n, *ps = p.part_sum + (size_t)c * n;
                 unsigned long long *lf = (unsigned long long *)(p.last_flipped + (size_t)c * n);
                 const int64_t lsum = (int64_t)p.labels[0] + (int64_t)p.labels[1];
-                if (lane == 0 && r0 && last_flip0 >= 0) {  // the run of the batch's start state goes on
-                    atomicMax(lf + last_flip0, (unsigned long long)(steps0 + r0));
-                    atomicAdd((unsigned long long *)(ps + last_flip0), (unsigned long long)((lsum - 2 * (int64_t)p.labels[a_last0]) * r0));
-                    atomicAdd((unsigned long long *)(nf + last_flip0), (unsigned long long)r0);
-                }
-                if (is_acc) {
-                    const int64_t t_last = t_acc + run_len - 1;
-                    atomicMax(lf + v, (unsigned long long)t_last);
-                    atomicAdd((unsigned long long *)(ps + v), (unsigned long long)((lsum - 2 * (int64_t)p.labels[1 - av]) * t_last));
-                    atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
-                }
+                const int64_t t_last = t_acc + run_len - 1;
+                atomicMax(lf + v, (unsigned long long)t_last);
+                atomicAdd((unsigned long long *)(ps + v), (unsigned long long)((lsum - 2 * (int64_t)p.labels[1 - av]) * t_last));
+                atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
             }
-            if ((p.diag & FC_DIAG_FLIPS_EXACT) && is_acc) {
+            if (!defer && (p.diag & FC_DIAG_FLIPS_EXACT) && is_acc) {
                 // the corrected companions: one count per accepted
                 // flip, the label's time integral as -(L_new - L_old) t per flip (+ L_now T at
                 // read-out, fc_run_read_flips_exact), the flip's yield; commuting updates only
@@ -873,7 +960,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 atomicAdd((unsigned long long *)(p.occ_acc + o), (unsigned long long)(-dl * t_acc));
                 atomicMax((unsigned long long *)(p.last_accept + o), (unsigned long long)t_acc);
             }
-            if ((p.diag & FC_DIAG_EDGES) && is_acc) {
+            if (!defer && (p.diag & FC_DIAG_EDGES) && is_acc) {
                 // cut_times[e] (yields with e cut, :383-384) = sum of the yields at which e turns
                 // uncut - sum of those at which it turns cut (+ the yield count while it is cut:
                 // fc_run_read_edges); commuting adds only
