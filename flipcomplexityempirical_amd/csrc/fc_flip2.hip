@@ -152,7 +152,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const int nbq = in ? (int)q_nb[lane] : 0;
             const int u = (int)(qv & 0xffffu), cq = (int)(qc & 0x7fffffffu), tg = (int)(qc >> 31);
             const uint32_t up = qv >> 16;  // neighbours in the old district: their edges turn cut
-            const int64_t lab_t = (int64_t)p.labels[tg], lab_o = (int64_t)p.labels[1 - tg];
+            // district labels: uniform loads (scalar), not per-lane gathers that would wait
+            // behind the atomics
+            const int64_t lab0 = p.labels[0], lab1 = p.labels[1];
+            const int64_t lab_t = tg ? lab1 : lab0, lab_o = tg ? lab0 : lab1;
             int eid[RMAX];
             if (in && (p.diag & FC_DIAG_EDGES)) {
                 const int4 *er = (const int4 *)(p.ring_eid + (size_t)u * RMAX);
@@ -208,14 +211,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     };
     auto wait_flush = [&]() {
         compiler_fence();
-        tally_flush();
         int64_t w = 0;
-        if (lane < qn) {
+        if (lane < qn) {  // the loads before the tallies' atomics (vmcnt completes in order)
             const uint64_t dq = q_d[lane];
             const Words4 g = philox4x32_10((uint32_t)dq, (uint32_t)(dq >> 32), chain_gid, 1u, p.seed_lo, p.seed_hi);
             w = geom_from(u53(g.x0, g.x1), p.log1mp[q_nb[lane]]);
             acc_wait += w * (int64_t)q_run[lane];
         }
+        tally_flush();
         wait_cur = (int64_t)(((uint64_t)(uint32_t)rl32((int)(uint32_t)w, qn - 1)) |
                              ((uint64_t)(uint32_t)rl32((int)(w >> 32), qn - 1) << 32));
         qn = 0;
@@ -877,10 +880,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb0], (unsigned long long)r0);
                 }
                 if ((p.diag & FC_DIAG_FLIPS) && last_flip0 >= 0) {
-                    const int64_t lsum = (int64_t)p.labels[0] + (int64_t)p.labels[1];
+                    const int64_t lab0 = p.labels[0], lab1 = p.labels[1];
                     const size_t o = (size_t)c * n + last_flip0;
                     atomicMax((unsigned long long *)(p.last_flipped + o), (unsigned long long)(steps0 + r0));
-                    atomicAdd((unsigned long long *)(p.part_sum + o), (unsigned long long)((lsum - 2 * (int64_t)p.labels[a_last0]) * r0));
+                    atomicAdd((unsigned long long *)(p.part_sum + o), (unsigned long long)((a_last0 ? lab0 - lab1 : lab1 - lab0) * r0));
                     atomicAdd((unsigned long long *)(p.num_flips + o), (unsigned long long)r0);
                 }
             }

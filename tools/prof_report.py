@@ -37,3 +37,6 @@ if S >= 24:
         b = max(x[5], 1)
         print(f"{g:3d} | {x[16]/max(x[17],1):8.0f} {x[17]/b:6.2f} | {x[18]/max(x[12],1):8.0f} {x[19]/max(x[12],1):8.0f} {x[21]/max(x[12],1):6.2f}")
 print("max chain total Mcyc", last[:, 0].max() / 1e6, "argmax", int(last[:, 0].argmax()))
+tot = last[:, 0]
+print("per group total Mcyc mean / p90 / max:",
+      " ".join(f"{g}:{tot[np.arange(C) % G == g].mean()/1e6:.1f}/{np.percentile(tot[np.arange(C) % G == g], 90)/1e6:.1f}/{tot[np.arange(C) % G == g].max()/1e6:.1f}" for g in range(G)))
