@@ -110,7 +110,9 @@ __device__ __forceinline__ bool district_rule(const int (&adv)[RMAX], uint32_t i
 }
 
 // KM = 2: two districts (BI_SIGN, and PAIR with k = 2, which coincide); the outer-face
-// exact rule applies.  KM = 0: k <= 32 districts, PAIR proposals, populations in LDS.
+// exact rule applies.  KM = 0: k <= 32 districts, PAIR proposals, populations in LDS.  KM = 1:
+// as KM = 0 with the workgroup-cooperative search (p.coop); a separate instance, because the
+// helper waves' code costs the common one its registers (C3: 14 -> 58 spilled VGPRs)
 // RMAX = 8: at most 128 VGPRs, four waves per SIMD (C3's 8192 chains per GPU run in two
 // rounds of waves instead of three: 1.46e9 against 1.35e9 proposals/s; a handful of VGPRs
 // spill, which costs C4's LDS-limited launch 2 %)
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     const int lane = (int)(threadIdx.x & 63u);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     // p.coop: one chain per workgroup; wave 0 runs it, waves 1.. join its contiguity searches
-    const bool coop = KM == 0 && p.coop != 0;
+    const bool coop = KM == 1 && p.coop != 0;  // only the KM = 1 instance carries the helper code
     const int c = coop ? (int)blockIdx.x : (int)blockIdx.x * (int)(blockDim.x >> 6) + wv;
     if (c >= p.n_chains) return;
 
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     bs.prof = nullptr;
     // [5][64]: node, word1, word2, draw offset, word3; with the district-graph rule the search
     // never runs and its scratch is not allocated (fc_run_create)
-    uint32_t *slot = KM == 0 && p.dgraph ? (uint32_t *)(T + (2 * RMAX + 2)) : (uint32_t *)(bs.nxt + p.words);
+    uint32_t *slot = KM != 2 && p.dgraph ? (uint32_t *)(T + (2 * RMAX + 2)) : (uint32_t *)(bs.nxt + p.words);
     int32_t *popk = (int32_t *)(slot + 5 * 64);    // [32] district populations (KM = 0)
     // accepted states whose geometric wait is still to be drawn (kWaitQK: creating draw, |B|
     // after the flip, yields so far); as in fc_flip2.hip, drained by wait_flush
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     int32_t *mcnt = (int32_t *)(q_run + kWaitQK);
     uint32_t *adj = (uint32_t *)(mcnt + p.k * p.k);
     int32_t *ngk = (int32_t *)(adj + 32);
-    const bool dgraph = KM == 0 && p.dgraph != 0;
+    const bool dgraph = KM != 2 && p.dgraph != 0;
     // cooperative search control words (coop implies no district tables: they start here)
     int32_t *ctl = (int32_t *)(q_run + kWaitQK);
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             ((uint4 *)fcnt)[i] = gf[i];
         }
         if (lane < 2 * RMAX + 1) T[lane] = p.thresh[(size_t)c * (2 * RMAX + 1) + lane];
-        if (KM == 0 && lane < 32) popk[lane] = p.popk[(size_t)c * 32 + lane];
+        if (KM != 2 && lane < 32) popk[lane] = p.popk[(size_t)c * 32 + lane];
         if (dgraph) {
             const int kk = p.k * p.k;
             for (int i = lane; i < kk; i += kWave) mcnt[i] = p.mcnt[(size_t)c * kk + i];
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             const int v = (int)(m >> 32);
             bool ok = inrange && (uint32_t)m >= p.lemire_thresh;
             bool hit;
-            if constexpr (KM == 0) {
+            if constexpr (KM != 2) {
                 // the draw's district slot r (word 3, exact Lemire over wmax) can only name a
                 // foreign district if r < fcnt[v] (foreign neighbours >= foreign districts):
                 // slots beyond are non-proposals whatever 1b would find, so they take no slot
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         // ring's A-runs that hold old neighbours: v + an X-path closes a Jordan curve with
         // old neighbours on both sides.  Anything else multi-run goes to the device BFS.
         bool s_cut = false;
-        if constexpr (KM == 0) {
+        if constexpr (KM != 2) {
             if (dgraph) {
                 // every multi-run case decided locally (district_rule above)
                 s_cut = has && !s_lin && nA > 0 && !district_rule<RMAX>(adv, inA, nbr, Ln, gam, av, adj);
@@ -484,9 +486,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             } else if (exact) {
                 okT = s_lin;
                 okN = gam ? s_cyc : s_lin;
-            } else if (KM == 0 && s_cut) {
+            } else if (KM != 2 && s_cut) {
                 okT = okN = false;
-            } else if (KM == 0 && dgraph) {
+            } else if (KM != 2 && dgraph) {
                 okT = okN = true;  // one run, or the district rule found the pieces joined
             } else {
                 known = s_lin;
@@ -556,7 +558,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             // non-hit draws to re-check below: nodes that entered the boundary; with PAIR
             // slots (KM = 0) any node whose foreign-neighbour count grew (its slot may now
             // fall below it)
-            uint64_t ent = __ballot(KM == 0 ? (is_nbr && dlt > 0) : enter);
+            uint64_t ent = __ballot(KM != 2 ? (is_nbr && dlt > 0) : enter);
             const int dnb = __popcll(__ballot(enter)) - __popcll(__ballot(leave));
             // district-graph tables: the pairs {vf, w} of vf's face-adjacent cells w move from
             // (Af, a[w]) to (tf, a[w]); a count crossing 0 flips an adjacency bit (as does an
@@ -596,7 +598,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             if (lane == 0) {
                 a[vf] = (int8_t)tf;
                 fcnt[vf] = (uint8_t)(__popc(nbrf) - __popc(tmf));
-                if constexpr (KM == 0) {
+                if constexpr (KM != 2) {
                     popk[Af] -= pvf;
                     popk[tf] += pvf;
                 }
@@ -842,7 +844,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             ga[i] = ((const uint4 *)a)[i];
             gf[i] = ((const uint4 *)fcnt)[i];
         }
-        if (KM == 0 && lane < 32) p.popk[(size_t)c * 32 + lane] = popk[lane];
+        if (KM != 2 && lane < 32) p.popk[(size_t)c * 32 + lane] = popk[lane];
         if (dgraph) {
             const int kk = p.k * p.k;
             for (int i = lane; i < kk; i += kWave) p.mcnt[(size_t)c * kk + i] = mcnt[i];
@@ -925,9 +927,17 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, siz
         default: return (int)hipErrorInvalidValue;    \
     }
     if (ring_max == 8) {
-        FC_NSUB_SWITCH(8, 0)
+        if (p.coop) {
+            FC_NSUB_SWITCH(8, 1)
+        } else {
+            FC_NSUB_SWITCH(8, 0)
+        }
     } else if (ring_max == 16) {
-        FC_NSUB_SWITCH(16, 0)
+        if (p.coop) {
+            FC_NSUB_SWITCH(16, 1)
+        } else {
+            FC_NSUB_SWITCH(16, 0)
+        }
     } else {
         return (int)hipErrorInvalidValue;
     }

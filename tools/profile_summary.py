@@ -2,6 +2,7 @@
 
   <tag>_bench.json          the bench line of the run
   <tag>_kernel_stats.csv    rocprofv3 --kernel-trace --stats of `bench.py --steps 5 --warmup 1`
+  <tag>_kernel_stats_full.csv  ... of the full-diagnostics leg (`--full-diag-steps 3`)
   <tag>_pmc_traffic.json    HBM bytes per launch of the flip kernel (also profiles/pmc_traffic.json,
                             which bench.py reads into roofline.traffic)
   <tag>_lds_issue.json      LDS / issue counters per dispatch
@@ -35,6 +36,8 @@ def flip_rows(path):
 bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
 json.dump(bench, open(os.path.join(dst, f"{tag}_bench.json"), "w"), indent=1)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+if os.path.exists(os.path.join(src, "trace_full", "run_kernel_stats.csv")):  # full-diagnostics leg
+    shutil.copy(os.path.join(src, "trace_full", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats_full.csv"))
 
 # per-launch durations of the headline kernel in the traced bench (steps 5, warmup 1)
 trace = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
