@@ -635,6 +635,7 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.n_chains = r->n_chains;
     k.k = r->p.k;
     k.popk = r->d_popk;
+    k.all_exact = r->g.n_exact == r->g.n ? 1 : 0;
     k.dgraph = r->dgraph ? 1 : 0;
     k.mcnt = r->d_mcnt;
     k.ngk = r->d_ngk;

@@ -36,7 +36,10 @@ namespace fc {
 
 using namespace dev;
 
-template <int RMAX, int NSUB, bool FULL>
+// SEARCH = false: every node is exact and FC_FLAG_FORCE_BFS is off (p.all_exact), so the run
+// rule decides every proposal and the instance carries no search code (its registers are the
+// hot loop's)
+template <int RMAX, int NSUB, bool FULL, bool SEARCH>
 __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const uint32_t vlink = (Ln >= 2 && (inA & 1u) && ((inA >> (Ln - 1)) & 1u)) ? (1u << (Ln - 1)) : 0u;
             s_cyc = one_run(nbrA, full & ~(lk | vlink), full);
         }
-        const bool exact = (rec.meta & kMetaExact) && !force_bfs;
+        const bool exact = SEARCH ? (rec.meta & kMetaExact) && !force_bfs : true;
         const bool gam = (rec.meta & kMetaGamma) != 0;
         const bool acc = mant53(w1, w2) < T[delta + RMAX];
         // per-slot predicates live as bits of one VGPR (st) through the commit; the compiler
@@ -696,7 +699,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     reeval(pos, -1, 0u);
                     continue;
                 }
-                if (u == pos) {
+                if (SEARCH && u == pos) {
                     const bool res = run_bfs(u);
                     if (lane == u) st |= ST_BD | (res ? ST_BR : 0u);
                 }
@@ -721,7 +724,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             rem -= nvalid;
             pos = f;
             if (f >= end) break;
-            if (!((VAL >> f) & 1ull)) {
+            if (SEARCH && !((VAL >> f) & 1ull)) {
                 const bool res = run_bfs(f);
                 if (lane == f) st |= ST_BD | (res ? ST_BR : 0u);
                 continue;
@@ -1097,18 +1100,27 @@ int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_
     // FULL: replay tapes, traces, event logs, histograms, per-node/per-edge tallies or a
     // hitting-time window; the lean instance keeps its registers for the hot loop.
     const bool full = p.tape || p.trace || (p.diag & ~(uint32_t)FC_DIAG_WAIT) || p.hit_lo <= p.hit_hi || p.variant;
-#define FC_LAUNCH2(R, S, F)                                                                             \
+    // no search code when the run rule decides every proposal (all nodes exact, no forced search)
+    const bool search = !p.all_exact || (p.flags & FC_FLAG_FORCE_BFS);
+#define FC_LAUNCH2(R, S, F, X)                                                                          \
     do {                                                                                                \
         if (lds > 65536)                                                                                \
-            (void)hipFuncSetAttribute((const void *)flip2_kernel<R, S, F>,                              \
+            (void)hipFuncSetAttribute((const void *)flip2_kernel<R, S, F, X>,                           \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
-        if (name) snprintf(name, name_cap, "fc::flip2_kernel<%d, %d, %s>", R, S, F ? "true" : "false"); \
-        hipLaunchKernelGGL((flip2_kernel<R, S, F>), grid, block, lds, s, p);                            \
+        if (name)                                                                                       \
+            snprintf(name, name_cap, "fc::flip2_kernel<%d, %d, %s, %s>", R, S, F ? "true" : "false",   \
+                     X ? "true" : "false");                                                             \
+        hipLaunchKernelGGL((flip2_kernel<R, S, F, X>), grid, block, lds, s, p);                         \
+    } while (0)
+#define FC_SEARCH2(R, S, F)                    \
+    do {                                       \
+        if (search) FC_LAUNCH2(R, S, F, true);  \
+        else FC_LAUNCH2(R, S, F, false);        \
     } while (0)
 #define FC_FULL2(R, S)                   \
     do {                                 \
-        if (full) FC_LAUNCH2(R, S, true);  \
-        else FC_LAUNCH2(R, S, false);      \
+        if (full) FC_SEARCH2(R, S, true);  \
+        else FC_SEARCH2(R, S, false);      \
     } while (0)
 #define FC_NSUB2(R)                                \
     switch (p.nsub) {                              \
@@ -1126,6 +1138,7 @@ int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_
     }
 #undef FC_NSUB2
 #undef FC_FULL2
+#undef FC_SEARCH2
 #undef FC_LAUNCH2
     return (int)hipGetLastError();
 }

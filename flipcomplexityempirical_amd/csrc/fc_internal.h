@@ -138,6 +138,7 @@ struct KParams {
     // k > 2 district-graph contiguity rule (every node exact, planar, simple outer face,
     // k <= kMaxKDistrictRule): per chain, face-adjacent cell pairs per district pair and
     // outer-face nodes per district (fc_kernels.hip district_rule)
+    int32_t all_exact;          // every node's contiguity is decided by the local rules (k = 2 run rule)
     int32_t dgraph;
     int32_t *mcnt;              // [n_chains * k * k] pair counts, cell [min(X, Y) * k + max(X, Y)]
     int32_t *ngk;               // [n_chains * 32] outer-face nodes per district
