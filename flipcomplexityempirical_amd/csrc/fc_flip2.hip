@@ -38,9 +38,11 @@ using namespace dev;
 
 // SEARCH = false: every node is exact and FC_FLAG_FORCE_BFS is off (p.all_exact), so the run
 // rule decides every proposal and the instance carries no search code (its registers are the
-// hot loop's)
-template <int RMAX, int NSUB, bool FULL, bool SEARCH>
+// hot loop's).  XTRA (FULL only): replay tapes, per-proposal traces, accept / constraint
+// variants and frozen nodes; the diagnostics instance without them keeps its registers too.
+template <int RMAX, int NSUB, bool FULL, bool SEARCH, bool XTRA>
 __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams p) {
+    static_assert(FULL || !XTRA, "XTRA is a FULL instance");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -101,13 +103,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     int stuck = 0;
     int rem = (int)p.n_steps;  // steps still to take in this launch (host: n_steps < 2^31)
     uint64_t draw_cap = draw + (uint64_t)p.max_draws;
-    if (FULL && p.tape && draw_cap > (uint64_t)p.tape_draws) draw_cap = (uint64_t)p.tape_draws;
+    if (XTRA && p.tape && draw_cap > (uint64_t)p.tape_draws) draw_cap = (uint64_t)p.tape_draws;
     const uint32_t chain_gid = p.chain_id_offset + (uint32_t)c;
     const bool force_bfs = (p.flags & FC_FLAG_FORCE_BFS) != 0;
     const bool want_wait = (p.diag & FC_DIAG_WAIT) != 0;
-    const bool trace_on = FULL && p.trace && c < p.trace_chains;
-    // waits drawn later from the queue (wait_flush) unless a trace or a replay tape needs them per batch
-    const bool defer = want_wait && !trace_on && !(FULL && p.tape);
+    const bool trace_on = XTRA && p.trace && c < p.trace_chains;
+    // accepted states queued (wait_flush: their waits drawn, FULL: their tallies applied later)
+    // unless a trace or a replay tape needs the waits per batch
+    const bool defer = (want_wait || FULL) && !trace_on && !(XTRA && p.tape);
 
     // per-lane accumulators, reduced once per launch
     int64_t acc_cut = 0, acc_nb = 0, acc_wait = 0, acc_cut2 = 0, acc_nb2 = 0;
@@ -214,8 +217,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     };
     auto wait_flush = [&]() {
         compiler_fence();
-        int64_t w = 0;
-        if (lane < qn) {  // the loads before the tallies' atomics (vmcnt completes in order)
+        int64_t w = 0;  // (waits off: 0, as the per-batch form leaves them)
+        if (want_wait && lane < qn) {  // the loads before the tallies' atomics (vmcnt completes in order)
             const uint64_t dq = q_d[lane];
             const Words4 g = philox4x32_10((uint32_t)dq, (uint32_t)(dq >> 32), chain_gid, 1u, p.seed_lo, p.seed_hi);
             w = geom_from(u53(g.x0, g.x1), p.log1mp[q_nb[lane]]);
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const bool inrange = (uint64_t)off < room;
             const uint64_t dr = draw + (uint64_t)off;
             Words4 w;
-            if (FULL && p.tape) {
+            if (XTRA && p.tape) {
                 const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + (inrange ? dr : draw)) * 6;
                 w = Words4{t[0], t[1], t[2], t[3]};
             } else {
@@ -364,7 +367,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // would otherwise hold each as a 64-bit lane mask in SGPRs for the whole loop
         uint32_t st = (hit ? LF_HIT : 0u) | (acc ? LF_ACC : 0u) | (s_lin ? LF_SLIN : 0u) | (s_cyc ? LF_SCYC : 0u) |
                       (exact ? LF_EXACT : 0u) | (gam ? LF_GAM : 0u) | (has ? LF_HAS : 0u);
-        if (FULL && (rec.meta & kMetaFrozen)) st |= LF_FRZ;
+        if (XTRA && (rec.meta & kMetaFrozen)) st |= LF_FRZ;
         FC_STAMP(t_c);
         FC_PROF(2, t_c - t_b);
 
@@ -489,7 +492,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             bool valid = prop & known & ok & popok;
             bool acc_now = acc;
             bool inv_contig = !ok;  // reason of an invalid proposal: contiguity, else "pop"
-            if constexpr (FULL) {
+            if constexpr (XTRA) {
                 if (p.variant) {
                     // Validator members re-draw, accept-callable constraints reject the step
                     // (grid_chain_sec11.py:39-52,81-110,159-165); contiguity / populations as
@@ -849,9 +852,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         const int first_acc = ACCM ? __builtin_ctzll(ACCM) : end;
         const int r0 = __popcll(VSM & bits_below(first_acc));
         int64_t my_wait = 0;
-        if (FULL && want_wait && !defer && is_acc) {
+        if (XTRA && want_wait && !defer && is_acc) {
             Words4 g;
-            if (FULL && p.tape) {
+            if (XTRA && p.tape) {
                 const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + d) * 6;
                 g = Words4{t[4], t[5], 0u, 0u};
             } else {
@@ -912,7 +915,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             }
         }
         if constexpr (FULL) {
-            if (!defer && (p.diag & FC_DIAG_SERIES) && ACCM) {
+            // per batch only with a trace or a tape (XTRA); else in tally_flush
+            if (XTRA && !defer && (p.diag & FC_DIAG_SERIES) && ACCM) {
                 const int64_t idx = ev_len + __popcll(ACCM & bits_below(ln));
                 if (is_acc && idx < p.ev_cap) {
                     fc_event ev;
@@ -934,11 +938,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 }
             }
             // per batch only when the queue is off (trace, tape): else tally_flush
-            if (!defer && (p.diag & FC_DIAG_HIST) && is_acc) {
+            if (XTRA && !defer && (p.diag & FC_DIAG_HIST) && is_acc) {
                 atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
                 atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb_after], (unsigned long long)run_len);
             }
-            if (!defer && (p.diag & FC_DIAG_FLIPS) && is_acc) {
+            if (XTRA && !defer && (p.diag & FC_DIAG_FLIPS) && is_acc) {
                 // part.flips is stale on rejected steps: every yield of a run repeats the update
                 // part_sum[f] -= a[f] * (t - last_flipped[f]) for the node f whose flip created
                 // the state (grid_chain_sec11.py:396-400).  With two districts a node's label
@@ -956,7 +960,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 atomicAdd((unsigned long long *)(ps + v), (unsigned long long)((lsum - 2 * (int64_t)p.labels[1 - av]) * t_last));
                 atomicAdd((unsigned long long *)(nf + v), (unsigned long long)run_len);
             }
-            if (!defer && (p.diag & FC_DIAG_FLIPS_EXACT) && is_acc) {
+            if (XTRA && !defer && (p.diag & FC_DIAG_FLIPS_EXACT) && is_acc) {
                 // the corrected companions: one count per accepted
                 // flip, the label's time integral as -(L_new - L_old) t per flip (+ L_now T at
                 // read-out, fc_run_read_flips_exact), the flip's yield; commuting updates only
@@ -966,7 +970,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 atomicAdd((unsigned long long *)(p.occ_acc + o), (unsigned long long)(-dl * t_acc));
                 atomicMax((unsigned long long *)(p.last_accept + o), (unsigned long long)t_acc);
             }
-            if (!defer && (p.diag & FC_DIAG_EDGES) && is_acc) {
+            if (XTRA && !defer && (p.diag & FC_DIAG_EDGES) && is_acc) {
                 // cut_times[e] (yields with e cut, :383-384) = sum of the yields at which e turns
                 // uncut - sum of those at which it turns cut (+ the yield count while it is cut:
                 // fc_run_read_edges); commuting adds only
@@ -1100,27 +1104,30 @@ int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_
     // FULL: replay tapes, traces, event logs, histograms, per-node/per-edge tallies or a
     // hitting-time window; the lean instance keeps its registers for the hot loop.
     const bool full = p.tape || p.trace || (p.diag & ~(uint32_t)FC_DIAG_WAIT) || p.hit_lo <= p.hit_hi || p.variant;
+    // replay tapes, traces, accept / constraint variants, frozen nodes
+    const bool xtra = p.tape || p.trace || p.variant;
     // no search code when the run rule decides every proposal (all nodes exact, no forced search)
     const bool search = !p.all_exact || (p.flags & FC_FLAG_FORCE_BFS);
-#define FC_LAUNCH2(R, S, F, X)                                                                          \
+#define FC_LAUNCH2(R, S, F, X, Y)                                                                       \
     do {                                                                                                \
         if (lds > 65536)                                                                                \
-            (void)hipFuncSetAttribute((const void *)flip2_kernel<R, S, F, X>,                           \
+            (void)hipFuncSetAttribute((const void *)flip2_kernel<R, S, F, X, Y>,                        \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
         if (name)                                                                                       \
-            snprintf(name, name_cap, "fc::flip2_kernel<%d, %d, %s, %s>", R, S, F ? "true" : "false",   \
-                     X ? "true" : "false");                                                             \
-        hipLaunchKernelGGL((flip2_kernel<R, S, F, X>), grid, block, lds, s, p);                         \
+            snprintf(name, name_cap, "fc::flip2_kernel<%d, %d, %s, %s, %s>", R, S, F ? "true" : "false", \
+                     X ? "true" : "false", Y ? "true" : "false");                                      \
+        hipLaunchKernelGGL((flip2_kernel<R, S, F, X, Y>), grid, block, lds, s, p);                      \
     } while (0)
-#define FC_SEARCH2(R, S, F)                    \
-    do {                                       \
-        if (search) FC_LAUNCH2(R, S, F, true);  \
-        else FC_LAUNCH2(R, S, F, false);        \
+#define FC_SEARCH2(R, S, F, Y)                    \
+    do {                                          \
+        if (search) FC_LAUNCH2(R, S, F, true, Y);  \
+        else FC_LAUNCH2(R, S, F, false, Y);        \
     } while (0)
-#define FC_FULL2(R, S)                   \
-    do {                                 \
-        if (full) FC_SEARCH2(R, S, true);  \
-        else FC_SEARCH2(R, S, false);      \
+#define FC_FULL2(R, S)                                \
+    do {                                              \
+        if (xtra) FC_SEARCH2(R, S, true, true);        \
+        else if (full) FC_SEARCH2(R, S, true, false);  \
+        else FC_SEARCH2(R, S, false, false);           \
     } while (0)
 #define FC_NSUB2(R)                                \
     switch (p.nsub) {                              \

@@ -203,7 +203,7 @@ def test_sec11_batch_shapes(gpu, cref, sec11, nsub, hit_stop, extra, lean):
     run.steps(1500)
     name = run.kernel_name()
     # sec11: every node exact, so the instance without search code (fourth parameter false)
-    assert f"flip2_kernel<8, {nsub}, {'false' if lean else 'true'}, false>" in name, name
+    assert f"flip2_kernel<8, {nsub}, {'false' if lean else 'true'}, false, " in name, name
     st = run.stats()
     fin = run.state()
     if not lean:
@@ -235,7 +235,7 @@ def test_sec11_lean_wait_queue(gpu, cref, sec11, launches, lean):
     run = FlipRun(fg, inits, cfg, bases=bases)
     for n in launches:
         run.steps(n)
-    assert f"flip2_kernel<8, 4, {'false' if lean else 'true'}, false>" in run.kernel_name()
+    assert f"flip2_kernel<8, 4, {'false' if lean else 'true'}, false, " in run.kernel_name()
     st = run.stats()
     total = sum(launches)
     for c in range(20):

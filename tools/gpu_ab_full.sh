@@ -5,7 +5,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 OUT=$R/gpurun_out; mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest tests/test_parity_gpu.py tests/test_corrected_stats_gpu.py tests/test_chain_gpu.py \
-  tests/test_checkpoint_gpu.py tests/test_series_gpu.py tests/test_slope_gpu.py -x -q -m gpu --timeout 300 --timeout-method thread > "$OUT/pytest_k2full.log" 2>&1
+  tests/test_checkpoint_gpu.py tests/test_series_gpu.py tests/test_slope_gpu.py tests/test_variants_gpu.py tests/test_node_tape_gpu.py -x -q -m gpu --timeout 300 --timeout-method thread > "$OUT/pytest_k2full.log" 2>&1
 rc=$?; tail -4 "$OUT/pytest_k2full.log"; [ $rc -eq 0 ] || exit $rc
 for rep in 1 2; do
   for D in ${DIAGS:-15 1}; do
