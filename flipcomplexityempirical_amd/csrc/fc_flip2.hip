@@ -36,6 +36,13 @@ namespace fc {
 
 using namespace dev;
 
+// The queued waits' inversion, out of line: inlined, the f64 log's polynomial constants were
+// hoisted out of the batch loop into VGPRs that the whole loop then carried (and spilled); the
+// call runs once per queue drain.
+__device__ __attribute__((noinline)) int64_t geom_wait_of(uint32_t x0, uint32_t x1, double log1mp) {
+    return geom_from(u53(x0, x1), log1mp);
+}
+
 // SEARCH = false: every node is exact and FC_FLAG_FORCE_BFS is off (p.all_exact), so the run
 // rule decides every proposal and the instance carries no search code (its registers are the
 // hot loop's).  XTRA (FULL only): replay tapes, per-proposal traces, accept / constraint
@@ -221,7 +228,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         if (want_wait && lane < qn) {  // the loads before the tallies' atomics (vmcnt completes in order)
             const uint64_t dq = q_d[lane];
             const Words4 g = philox4x32_10((uint32_t)dq, (uint32_t)(dq >> 32), chain_gid, 1u, p.seed_lo, p.seed_hi);
-            w = geom_from(u53(g.x0, g.x1), p.log1mp[q_nb[lane]]);
+            w = geom_wait_of(g.x0, g.x1, p.log1mp[q_nb[lane]]);
             acc_wait += w * (int64_t)q_run[lane];
         }
         tally_flush();
