@@ -569,5 +569,12 @@ constexpr uint32_t LF_HAS = 1u << 14;    // the lane holds a slot
 constexpr uint32_t LF_WROTE = 1u << 15;  // the lane holds commit marks
 constexpr uint32_t LF_FRZ = 1u << 16;    // FC_CON_FIXED: the node may not flip
 
+// The queued waits' inversion (geom_wait, grid_chain_sec11.py:147-148), out of line: inlined
+// into a flip kernel, the f64 log's polynomial constants were hoisted out of the batch loop into
+// VGPRs that the whole loop then carried (and spilled); the call runs once per queue drain.
+__device__ __attribute__((noinline)) inline int64_t geom_wait_of(uint32_t x0, uint32_t x1, double log1mp) {
+    return geom_from(u53(x0, x1), log1mp);
+}
+
 }  // namespace dev
 }  // namespace fc

@@ -36,12 +36,6 @@ namespace fc {
 
 using namespace dev;
 
-// The queued waits' inversion, out of line: inlined, the f64 log's polynomial constants were
-// hoisted out of the batch loop into VGPRs that the whole loop then carried (and spilled); the
-// call runs once per queue drain.
-__device__ __attribute__((noinline)) int64_t geom_wait_of(uint32_t x0, uint32_t x1, double log1mp) {
-    return geom_from(u53(x0, x1), log1mp);
-}
 
 // SEARCH = false: every node is exact and FC_FLAG_FORCE_BFS is off (p.all_exact), so the run
 // rule decides every proposal and the instance carries no search code (its registers are the
