@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "fc_internal.h"
+#include "fc_philox.h"
 #include "fc_ring.h"
 
 namespace fc {
