@@ -112,7 +112,8 @@ __device__ __forceinline__ bool district_rule(const int (&adv)[RMAX], uint32_t i
 // KM = 2: two districts (BI_SIGN, and PAIR with k = 2, which coincide); the outer-face
 // exact rule applies.  KM = 0: k <= 32 districts, PAIR proposals, populations in LDS.  KM = 1:
 // as KM = 0 with the workgroup-cooperative search (p.coop); a separate instance, because the
-// helper waves' code costs the common one its registers (C3: 14 -> 58 spilled VGPRs)
+// helper waves' code costs the common one its registers (C3: 14 -> 58 spilled VGPRs).  KM = 3:
+// as KM = 0 when the district-graph rule decides every proposal (p.dgraph): no search code.
 // RMAX = 8: at most 128 VGPRs, four waves per SIMD (C3's 8192 chains per GPU run in two
 // rounds of waves instead of three: 1.46e9 against 1.35e9 proposals/s; a handful of VGPRs
 // spill, which costs C4's LDS-limited launch 2 %)
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     int32_t *mcnt = (int32_t *)(q_run + kWaitQK);
     uint32_t *adj = (uint32_t *)(mcnt + p.k * p.k);
     int32_t *ngk = (int32_t *)(adj + 32);
-    const bool dgraph = KM != 2 && p.dgraph != 0;
+    const bool dgraph = KM == 3 || (KM != 2 && p.dgraph != 0);  // KM = 3: always, by construction
     // cooperative search control words (coop implies no district tables: they start here)
     int32_t *ctl = (int32_t *)(q_run + kWaitQK);
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             rem -= nvalid;
             pos = f;
             if (f >= end) break;
-            if (!((VAL >> f) & 1ull)) {
+            if (KM != 3 && !((VAL >> f) & 1ull)) {
                 // undecided contiguity at slot f: device BFS on the current state
                 const bool res = run_bfs(f);
                 if (lane == f) st |= ST_BD | (res ? ST_BR : 0u);
@@ -926,15 +927,20 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, siz
         case 4: FC_FULL_SWITCH(R, 4, K); break;       \
         default: return (int)hipErrorInvalidValue;    \
     }
+    // (p.dgraph is off under FC_FLAG_FORCE_BFS, and coop needs it off)
     if (ring_max == 8) {
         if (p.coop) {
             FC_NSUB_SWITCH(8, 1)
+        } else if (p.dgraph) {
+            FC_NSUB_SWITCH(8, 3)
         } else {
             FC_NSUB_SWITCH(8, 0)
         }
     } else if (ring_max == 16) {
         if (p.coop) {
             FC_NSUB_SWITCH(16, 1)
+        } else if (p.dgraph) {
+            FC_NSUB_SWITCH(16, 3)
         } else {
             FC_NSUB_SWITCH(16, 0)
         }
