@@ -238,3 +238,31 @@ def test_large_graph_search_workgroup_and_wave(gpu, cref, graph, waves):
     st = run.stats()
     assert int(st["bfs_calls"].sum()) > 0
     _check(cref, spec, run, k, inits, bases, steps=400, pct=0.1)
+
+
+def test_instance_selection_and_agreement(gpu, sec11):
+    """The district-graph rule decides every C3 proposal, so the launch takes the instance without
+    search code (KM = 3); FC_FLAG_FORCE_BFS takes the searching one (KM = 0).  Both are exact, so
+    their chains agree state for state; likewise k = 2 without (SEARCH = false) and with forced
+    search."""
+    k, n_chains, steps = 4, 16, 1200
+    a0 = sec11.assignment_array(G.quadrant_plan(sec11.nodes), list(range(k)))
+    inits = np.stack([a0] * n_chains)
+    bases = np.asarray([[0.5, 1.0, G.SEC11_MU, 3.0][c % 4] for c in range(n_chains)])
+    runs = [_run_pair(sec11, inits, bases, k, steps=steps, pct=0.05, flags=f) for f in (0, _lib.FC_FLAG_FORCE_BFS)]
+    assert runs[0].kernel_name().startswith("fc::flip_kernel<8, 2, 3, "), runs[0].kernel_name()
+    assert runs[1].kernel_name().startswith("fc::flip_kernel<8, 2, 0, "), runs[1].kernel_name()
+    assert runs[0].stats()["bfs_calls"].sum() == 0 and runs[1].stats()["bfs_calls"].sum() > 0
+    for key in ("steps", "proposals", "accepted", "sum_cut", "sum_nb", "sum_wait", "cut", "nb"):
+        assert np.array_equal(runs[0].stats()[key], runs[1].stats()[key]), key
+    assert np.array_equal(runs[0].state(), runs[1].state())
+    i2 = np.stack([sec11.assignment_array(G.sec11_plan(c % 3, sec11.nodes), [-1, 1]) for c in range(n_chains)])
+    b2 = np.asarray([G.SEC11_BASES[c % 10] for c in range(n_chains)])
+    r2 = [_run_pair(sec11, i2, b2, 2, steps=steps, pct=0.1, flags=f, proposal=_lib.FC_PROPOSE_BI_SIGN)
+          for f in (0, _lib.FC_FLAG_FORCE_BFS)]
+    # (every chain traced: the XTRA diagnostics instance, SEARCH the fourth parameter)
+    assert r2[0].kernel_name().endswith(", true, false, true>"), r2[0].kernel_name()
+    assert r2[1].kernel_name().endswith(", true, true, true>"), r2[1].kernel_name()
+    for key in ("steps", "proposals", "accepted", "sum_cut", "sum_nb", "sum_wait", "cut", "nb"):
+        assert np.array_equal(r2[0].stats()[key], r2[1].stats()[key]), key
+    assert np.array_equal(r2[0].state(), r2[1].state())
