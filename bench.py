@@ -328,25 +328,41 @@ def main():
         # kernel turns the log into per-event slope / angle, copied to the host as the
         # reference's lists (in chunks of chains)
         series = args.workload == "c2"
+        # C4 (BASELINE config 4): the |cut| trace's autocorrelation at lags 1 .. 2^16 and the
+        # hitting time of a target |cut| (10 % above the lowest start), on the device, per launch
+        c4diag = args.workload == "c4"
         full = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
-        if series:
+        if series or c4diag:
             full |= _lib.FC_DIAG_SERIES
+        hit = (-1, -2)
+        if c4diag:
+            cut0 = min(G.cut_and_boundary(spec, inits[c])[0] for c in range(0, len(inits), max(1, len(inits) // 64)))
+            hit = (int(np.ceil(1.1 * cut0)), 10 ** 9)
         cfg_f = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
                           chain_id_offset=int(off), device=local_rank, diag_mask=full, tune=tune,
-                          event_cap=args.chain_steps + 1 if series else 0)
+                          event_cap=args.chain_steps + 1 if (series or c4diag) else 0, hit_lo=hit[0], hit_hi=hit[1])
+        lags = [1 << i for i in range(17)]
         rf = FlipRun(fg, inits, cfg_f, bases=bases)
         frame = G.slope_frame(spec, "sec11") if series else None
         rf.steps(args.chain_steps)
         barrier_sync_f = lambda: (rf.sync(), dist.barrier() if dist is not None else None)  # noqa: E731
-        if series:
+        if series or c4diag:
             rf.series_reset()
         barrier_sync_f()
         f0 = rf.stats()
         rf.timings()
         t_series, n_events, n_nan = 0.0, 0, 0
+        t_acf, acf1 = 0.0, []
         t0f = time.perf_counter()
         for _ in range(args.full_diag_steps):
             rf.steps(args.chain_steps)
+            if c4diag:
+                rf.sync()
+                ts = time.perf_counter()
+                _, acf = rf.autocorr(lags)
+                acf1.append(float(np.nanmean(acf[:, 0])))
+                rf.series_reset()
+                t_acf += time.perf_counter() - ts
             if series:
                 rf.sync()  # the launch is asynchronous: its time must not land in t_series
                 ts = time.perf_counter()
@@ -369,12 +385,15 @@ def main():
         pf = float(D.allreduce_sum(np.asarray([pf]), dist, dev)[0])
         yields = int(red["scalars"][:, D.AGG_FIELDS.index("steps")].sum()) + C * world
         t_series = D.allreduce_max(t_series, dist, dev)
-        full_out = {"value": pf / (dtf - t_series), "unit": "proposals/s", "launches": args.full_diag_steps,
+        t_acf = D.allreduce_max(t_acf, dist, dev)
+        full_out = {"value": pf / (dtf - t_series - t_acf), "unit": "proposals/s", "launches": args.full_diag_steps,
                     "value_with_frame_series_on_host": pf / dtf if series else None,
                     "kernel": rf.kernel_name(), "kernel_ms": kf,
                     "diag": "waits + cut/|B| histograms + per-edge cut_times + per-node flips"
                             + (" + accepted-flip log -> per-event slope / angle on the device, copied to "
                                "the host" if series else "")
+                            + (" + accepted-flip log -> |cut| autocorrelation and hitting time on the device"
+                               if c4diag else "")
                             + " (the reference loop body, grid_chain_sec11.py:367-400)",
                     "frame_series": {"ms_per_launch": t_series / max(args.full_diag_steps, 1) * 1e3,
                                      "events": n_events, "events_per_s": n_events / t_series if t_series else None,
@@ -382,6 +401,12 @@ def main():
                                      "note": "fc_run_frame_series over all chains in chunks of 256, per-event "
                                              "slope / angle / frame-cut count copied to host arrays"}
                     if series else None,
+                    "c4_series": {"hit_window": list(hit), "hit_fraction": float((f1["hit_time"] >= 0).mean()),
+                                  "lags": lags, "mean_acf_lag1": acf1,
+                                  "autocorr_ms_per_launch": t_acf / max(args.full_diag_steps, 1) * 1e3,
+                                  "note": "fc_run_autocorr (event log -> per-yield |cut| -> exact lag sums) "
+                                          "after every launch, results copied to the host"}
+                    if c4diag else None,
                     "reduced": {"ranks": world, "collectives": "allreduce SUM (scalars, histograms, cut_times, "
                                 "num_flips, part_sum) + allreduce MAX (last_flipped)",
                                 "yields": yields, "cut_hist_mass": int(red["cut_hist"].sum()),

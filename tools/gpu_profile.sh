@@ -18,7 +18,9 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc_lds" -o pmc --output-format csv -- python3 $BENCH > "$OUT/pmc_lds.log" 2>&1 || { echo "pmc lds failed"; tail -20 "$OUT/pmc_lds.log"; exit 1; }
 for w in c3 c4 c5; do
-  timeout -k 10 300 python3 bench.py --workload $w --steps 5 --warmup 1 --chain-steps 20000 --no-cpu-baseline --full-diag-steps 0 > "$OUT/side_$w.json" 2> "$OUT/side_$w.err" || { echo "side $w failed"; tail -20 "$OUT/side_$w.err"; exit 1; }
+  # C4 also runs its diagnostics leg (event log, hitting time, autocorrelation; BASELINE config 4)
+  FD=0; [ $w = c4 ] && FD=2
+  timeout -k 10 300 python3 bench.py --workload $w --steps 5 --warmup 1 --chain-steps 20000 --no-cpu-baseline --full-diag-steps $FD > "$OUT/side_$w.json" 2> "$OUT/side_$w.err" || { echo "side $w failed"; tail -20 "$OUT/side_$w.err"; exit 1; }
   cat "$OUT/side_$w.json"
 done
 echo PROFILE_OK
