@@ -36,7 +36,6 @@ namespace fc {
 
 using namespace dev;
 
-
 // SEARCH = false: every node is exact and FC_FLAG_FORCE_BFS is off (p.all_exact), so the run
 // rule decides every proposal and the instance carries no search code (its registers are the
 // hot loop's).  XTRA (FULL only): replay tapes, per-proposal traces, accept / constraint
