@@ -11,7 +11,10 @@ alignment-2 plan, pop tolerance 0.1, bases 0.8 and mu; 200 chains per base, T = 
 plus the district-shape statistics of the driver's slope / angle lines (:371-394): each
 chain's mean angle over the yields with exactly two frame cut edges, the end state's angle,
 and the fraction of such yields.
-Run: python tests/golden/make_native.py  (about 1.5 min on 8 cores)."""
+native_rng_sec11_long.npz: as sec11 with the alignment-0 plan, the extreme bases 0.2 and 10
+and T = 10,000 steps (200 chains per base): long chains far from the start state.
+Run: python tests/golden/make_native.py [c1 sec11 sec11_long]  (c1 + sec11 about 1.5 min on
+8 cores, sec11_long about 10 min)."""
 import os
 import sys
 from concurrent.futures import ProcessPoolExecutor
@@ -21,7 +24,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
-CONFIGS = {"c1": ([1.0, 2.63815853], 400, 2000), "sec11": ([0.8, 2.63815853], 200, 1000)}
+CONFIGS = {"c1": ([1.0, 2.63815853], 400, 2000), "sec11": ([0.8, 2.63815853], 200, 1000),
+           "sec11_long": ([0.2, 10.0], 200, 10000)}
+ALIGNMENT = {"sec11": 2, "sec11_long": 0}  # sec11 start plan (grid_chain_sec11.py:195-214)
 
 
 SHAPE = ("angle_mean", "angle_end", "frame2_frac")  # sec11 only (the reference's frame)
@@ -48,7 +53,7 @@ def one(args):
         plan = G.threshold_plan(spec.nodes, 0, 5)
     else:
         spec = G.sec11_graph()
-        plan = G.sec11_plan(2, spec.nodes)
+        plan = G.sec11_plan(ALIGNMENT[cfg], spec.nodes)
     (lo, hi), _ = G.population_bounds(spec.n, 2, 0.1)
     ch = NativeRngChain(spec, plan, base=base, pop_bounds=(lo, hi), seed=1000 + i, log1mp=G.log1mp_table(spec.n, 2))
     shape = ()
@@ -81,7 +86,7 @@ def main(which=None):
         with ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
             for bi, b in enumerate(bases):
                 r = np.asarray(list(ex.map(one, [(cfg, b, i, T) for i in range(M)])), dtype=np.float64)
-                names = ("cut", "nb", "pop1", "wait", "mean_cut", "mean_nb") + (SHAPE if cfg == "sec11" else ())
+                names = ("cut", "nb", "pop1", "wait", "mean_cut", "mean_nb") + (SHAPE if cfg != "c1" else ())
                 for j, name in enumerate(names):
                     out[f"b{bi}_{name}"] = r[:, j]
         np.savez_compressed(os.path.join(os.path.dirname(os.path.abspath(__file__)), f"native_rng_{cfg}.npz"), **out)

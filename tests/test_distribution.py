@@ -7,7 +7,9 @@ tests/golden/make_native.py) against the canonical Philox stream of the C oracle
   c1:    BASELINE config C1 (10x10 grid, k = 2, plan x[0] >= 5, pop tolerance 0.1),
          bases 1 and mu, 2000 steps;
   sec11: the headline lattice (grid_chain_sec11.py:186-260), alignment-2 plan, pop
-         tolerance 0.1, bases 0.8 and mu, 1000 steps.
+         tolerance 0.1, bases 0.8 and mu, 1000 steps;
+  sec11_long: alignment-0 plan, the extreme bases 0.2 and 10, 10,000 steps (long chains far
+         from the start state).
 Two-sample KS tests on the end state's |cut edges|, |b_nodes| and district population, each
 chain's time-averaged |cut| and |B|, and the geometric wait of the end state; for sec11 also
 the district-shape statistics of the driver's slope / angle lines (grid_chain_sec11.py:55-78,
@@ -28,7 +30,8 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 STATS = ("cut", "nb", "pop1", "wait", "mean_cut", "mean_nb")
 SHAPE_STATS = ("angle_mean", "angle_end")  # sec11 only
 P_MIN = 1e-3  # per comparison; the samples are fixed (seeded), so the outcome is deterministic
-CASES = [("c1", 0), ("c1", 1), ("sec11", 0), ("sec11", 1)]
+CASES = [("c1", 0), ("c1", 1), ("sec11", 0), ("sec11", 1), ("sec11_long", 0), ("sec11_long", 1)]
+ALIGNMENT = {"sec11": 2, "sec11_long": 0}
 
 
 def fixture(cfg):
@@ -41,7 +44,7 @@ def setup(cfg):
         a0 = spec.assignment_array(G.threshold_plan(spec.nodes, 0, 5), [-1, 1])
     else:
         spec = G.sec11_graph()
-        a0 = spec.assignment_array(G.sec11_plan(2, spec.nodes), [-1, 1])
+        a0 = spec.assignment_array(G.sec11_plan(ALIGNMENT[cfg], spec.nodes), [-1, 1])
     _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
     return spec, a0, lo, hi
 
@@ -102,9 +105,9 @@ def test_canonical_oracle_matches_native_rng(cref, cfg, bi):
     T, base = int(fix["T"]), float(fix["bases"][bi])
     spec, a0, lo, hi = setup(cfg)
     from oracle.flipref import events_from_trace
-    frame = G.slope_frame(spec, "sec11") if cfg == "sec11" else None
+    frame = G.slope_frame(spec, "sec11") if cfg != "c1" else None
     finals, waits, sc, sn, am, ae = [], [], [], [], [], []
-    for c in range(600):
+    for c in range(600 if T <= 2000 else 150):
         r = cref.run(spec, a0, base=base, pop_lo=lo, pop_hi=hi, seed=0xD15, chain_id=c, n_steps=T,
                      log1mp=G.log1mp_table(spec.n, 2), trace_cap=64 * T if frame is not None else 0)
         finals.append(r["final"])

@@ -17,7 +17,7 @@ def test_device_matches_native_rng(gpu, cfg, bi):
     T, base = int(fix["T"]), float(fix["bases"][bi])
     spec, a0, lo, hi = setup(cfg)
     C = 4096
-    shape = cfg == "sec11"
+    shape = cfg != "c1"
     diag = _lib.FC_DIAG_WAIT | (_lib.FC_DIAG_SERIES if shape else 0)
     run = FlipRun(FlipGraph(spec), np.stack([a0] * C),
                   RunConfig(seed=0xD15C0 + bi, pop_lo=lo, pop_hi=hi, base=base, diag_mask=diag,
@@ -29,16 +29,19 @@ def test_device_matches_native_rng(gpu, cfg, bi):
         # the interface angle after every accepted flip, from the device's frame-series kernel
         # (fc_run_frame_series: boundary_slope + the driver's angle line), weighted by the
         # yields each state lasts
-        fs = run.frame_series(G.slope_frame(spec, "sec11"))
+        frame = G.slope_frame(spec, "sec11")
         am, ae = np.full(C, np.nan), np.full(C, np.nan)
-        for c in range(C):
-            ev = run.events(c)
-            n = int(fs["len"][c])
-            assert n == ev.size + 1
-            w = np.diff(np.concatenate([[0], ev["t"], [T + 1]]))
-            ang, two = fs["angle"][c, :n], fs["n_cut"][c, :n] == 2
-            if two.any():
-                am[c] = float(np.sum(ang[two] * w[two]) / np.sum(w[two]))
-            ae[c] = ang[-1] if two[-1] else np.nan
+        for c0 in range(0, C, 1024):  # chunks of chains (10,000-step windows: 10^4 events each)
+            fs = run.frame_series(frame, chains=range(c0, c0 + 1024))
+            for j in range(1024):
+                c = c0 + j
+                ev = run.events(c)
+                n = int(fs["len"][j])
+                assert n == ev.size + 1
+                w = np.diff(np.concatenate([[0], ev["t"], [T + 1]]))
+                ang, two = fs["angle"][j, :n], fs["n_cut"][j, :n] == 2
+                if two.any():
+                    am[c] = float(np.sum(ang[two] * w[two]) / np.sum(w[two]))
+                ae[c] = ang[-1] if two[-1] else np.nan
         got["angle_mean"], got["angle_end"] = am, ae
     assert_same_distribution(fix, bi, got, f"device {cfg}")
