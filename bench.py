@@ -332,8 +332,10 @@ def main():
         # hitting time of a target |cut| (10 % above the lowest start), on the device, per launch
         c4diag = args.workload == "c4"
         full = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
-        if series or c4diag:
+        if series:
             full |= _lib.FC_DIAG_SERIES
+        if c4diag:  # the config's own diagnostics: the accepted-flip log (ACF) and the hitting time
+            full = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_SERIES
         hit = (-1, -2)
         if c4diag:
             cut0 = min(G.cut_and_boundary(spec, inits[c])[0] for c in range(0, len(inits), max(1, len(inits) // 64)))
@@ -376,10 +378,13 @@ def main():
         dtf = D.allreduce_max(time.perf_counter() - t0f, dist, dev)
         kf = D.allreduce_max(float(rf.timings().mean()), dist, dev)
         f1 = rf.stats()
-        ch, nh = rf.hist()
-        nf, ps, lf = rf.flips()
-        arrays = {"cut_hist": ch, "nb_hist": nh, "cut_times": rf.cut_times(), "num_flips": nf, "part_sum": ps,
-                  "last_flipped": lf}
+        arrays = {}
+        if full & _lib.FC_DIAG_HIST:
+            arrays["cut_hist"], arrays["nb_hist"] = rf.hist()
+        if full & _lib.FC_DIAG_EDGES:
+            arrays["cut_times"] = rf.cut_times()
+        if full & _lib.FC_DIAG_FLIPS:
+            arrays["num_flips"], arrays["part_sum"], arrays["last_flipped"] = rf.flips()
         red = D.allreduce_statistics(D.local_statistics(f1, gids % nb_, nb_, arrays), dist, dev)
         pf = float((f1["proposals"] - f0["proposals"]).sum())
         pf = float(D.allreduce_sum(np.asarray([pf]), dist, dev)[0])
@@ -389,12 +394,12 @@ def main():
         full_out = {"value": pf / (dtf - t_series - t_acf), "unit": "proposals/s", "launches": args.full_diag_steps,
                     "value_with_frame_series_on_host": pf / dtf if series else None,
                     "kernel": rf.kernel_name(), "kernel_ms": kf,
-                    "diag": "waits + cut/|B| histograms + per-edge cut_times + per-node flips"
-                            + (" + accepted-flip log -> per-event slope / angle on the device, copied to "
-                               "the host" if series else "")
-                            + (" + accepted-flip log -> |cut| autocorrelation and hitting time on the device"
-                               if c4diag else "")
-                            + " (the reference loop body, grid_chain_sec11.py:367-400)",
+                    "diag": ("waits + accepted-flip log -> |cut| autocorrelation and hitting time on the device "
+                             "(BASELINE config 4)" if c4diag else
+                             "waits + cut/|B| histograms + per-edge cut_times + per-node flips"
+                             + (" + accepted-flip log -> per-event slope / angle on the device, copied to "
+                                "the host" if series else "")
+                             + " (the reference loop body, grid_chain_sec11.py:367-400)"),
                     "frame_series": {"ms_per_launch": t_series / max(args.full_diag_steps, 1) * 1e3,
                                      "events": n_events, "events_per_s": n_events / t_series if t_series else None,
                                      "nan_angles": n_nan,
@@ -409,7 +414,7 @@ def main():
                     if c4diag else None,
                     "reduced": {"ranks": world, "collectives": "allreduce SUM (scalars, histograms, cut_times, "
                                 "num_flips, part_sum) + allreduce MAX (last_flipped)",
-                                "yields": yields, "cut_hist_mass": int(red["cut_hist"].sum()),
+                                "yields": yields, "cut_hist_mass": int(red["cut_hist"].sum()) if "cut_hist" in red else None,
                                 "checksums": D.checksums(red)}}
         rf.close()
 
