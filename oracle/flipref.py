@@ -134,10 +134,20 @@ class FrOutputs(ctypes.Structure):
 
 
 def build_lib(force: bool = False) -> str:
-    if force or not os.path.exists(LIB_PATH) or \
+    def stale():
+        return force or not os.path.exists(LIB_PATH) or \
             os.path.getmtime(LIB_PATH) < max(os.path.getmtime(os.path.join(HERE, f))
-                                             for f in ("flipref.c", "flipref.h", "recomref.c", "recomref.h")):
-        subprocess.run(["make", "-C", HERE, "-s"], check=True)
+                                             for f in ("flipref.c", "flipref.h", "recomref.c", "recomref.h"))
+    if stale():
+        import fcntl  # one build at a time (pytest-xdist workers share oracle/build)
+        os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+        with open(os.path.join(os.path.dirname(LIB_PATH), ".lock"), "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            try:
+                if stale():
+                    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+            finally:
+                fcntl.flock(lk, fcntl.LOCK_UN)
     return LIB_PATH
 
 

@@ -5,6 +5,7 @@ CSR + positions) and the plain-C oracle (``oracle/flipref.c``), compiled with
 lattices, the Delaunay workload and malformed CSR / position inputs.  Any sanitizer report
 aborts the harness (``-fno-sanitize-recover=all``), so a clean exit with the expected verdict
 is the pass condition.  CPU only."""
+import fcntl
 import os
 import shutil
 import subprocess
@@ -23,7 +24,14 @@ EXE = os.path.join(SAN, "build", "san_harness")
 def harness():
     if shutil.which("g++") is None or shutil.which("make") is None:
         pytest.skip("no host C++ toolchain")
-    subprocess.run(["make", "-s", "-C", SAN], check=True)
+    # one build at a time: pytest-xdist workers share tests/sanitize/build
+    os.makedirs(os.path.join(SAN, "build"), exist_ok=True)
+    with open(os.path.join(SAN, "build", ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            subprocess.run(["make", "-s", "-C", SAN], check=True)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     return EXE
 
 
