@@ -355,6 +355,7 @@ def main():
         rf.timings()
         t_series, n_events, n_nan = 0.0, 0, 0
         t_acf, acf1 = 0.0, []
+        fs_buf = None
         t0f = time.perf_counter()
         for _ in range(args.full_diag_steps):
             rf.steps(args.chain_steps)
@@ -368,10 +369,17 @@ def main():
             if series:
                 rf.sync()  # the launch is asynchronous: its time must not land in t_series
                 ts = time.perf_counter()
+                if fs_buf is None:  # host buffers reused over the chunks and launches
+                    cap_all = int(rf.stats()["events"].max()) + 1
+                    n_all = 256 * 2 * cap_all  # room for later launches' longer windows
+                    fs_buf = {"slope": np.empty(n_all), "angle": np.empty(n_all),
+                              "n_cut": np.empty(n_all, dtype=np.int32)}
                 for c0 in range(0, C, 256):
-                    fs = rf.frame_series(frame, chains=range(c0, min(C, c0 + 256)))
+                    fs = rf.frame_series(frame, chains=range(c0, min(C, c0 + 256)),
+                                         out={k: v.reshape(1, -1) for k, v in fs_buf.items()})
                     n_events += int(fs["len"].sum())
-                    n_nan += int(np.isnan(fs["angle"]).sum())  # padding entries are 0, not NaN
+                    live = np.arange(fs["angle"].shape[1])[None, :] < fs["len"][:, None]  # past len: padding
+                    n_nan += int(np.isnan(fs["angle"][live]).sum())
                 rf.series_reset()
                 t_series += time.perf_counter() - ts
         barrier_sync_f()

@@ -63,6 +63,9 @@ struct fc_run {
     int32_t *d_eu = nullptr, *d_ev = nullptr;  // recom: canonical edge list
     uint64_t *d_recom_thresh = nullptr;        // recom: [2E+1] acceptance thresholds
     int8_t *d_ser_a0 = nullptr;  // FC_DIAG_SERIES: assignment at the series window start
+    double *d_fs_out = nullptr;  // fc_run_frame_series output (slope, angle), grown on demand
+    int32_t *d_fs_cnt = nullptr; // ... frame-cut counts
+    size_t fs_cap = 0;           // entries per output array held
     char kname[96] = {0};        // last launched flip-kernel instance
     bool variant = false;        // accept / constraint variants (FULL k = 2 instance)
     struct {                     // fc_params.tune_* with the defaults filled in
@@ -103,7 +106,8 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh,
+                    r->d_fs_out, r->d_fs_cnt};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -1232,13 +1236,12 @@ int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, cons
         ev_len[c0 + i] = sc[i].ev_len;
         len[i] = sc[i].ev_len + 1;
     }
-    int32_t *d_fuv = nullptr, *d_tidx = nullptr, *d_cnt = nullptr;
+    int32_t *d_fuv = nullptr, *d_tidx = nullptr;
     int64_t *d_len = nullptr;
     uint64_t *d_tog = nullptr;
-    double *d_mid = nullptr, *d_out = nullptr;
+    double *d_mid = nullptr;
     auto cleanup = [&]() {
-        for (void *b : {(void *)d_fuv, (void *)d_tidx, (void *)d_cnt, (void *)d_len, (void *)d_tog, (void *)d_mid,
-                        (void *)d_out})
+        for (void *b : {(void *)d_fuv, (void *)d_tidx, (void *)d_len, (void *)d_tog, (void *)d_mid})
             if (b) (void)hipFree(b);
     };
     auto run = [&]() -> int {
@@ -1249,8 +1252,19 @@ int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, cons
         if ((q = dalloc(&d_tog, std::max<size_t>(tog.size(), 4)))) return q;
         if ((q = dalloc(&d_mid, (size_t)2 * std::max(n_frame, 1)))) return q;
         if ((q = dalloc(&d_len, (size_t)r->n_chains))) return q;
-        if ((q = dalloc(&d_out, 2 * outn))) return q;
-        if ((q = dalloc(&d_cnt, outn))) return q;
+        // the large outputs are kept by the run (chunked callers ask for similar sizes)
+        if (outn > r->fs_cap) {
+            if (r->d_fs_out) (void)hipFree(r->d_fs_out);
+            if (r->d_fs_cnt) (void)hipFree(r->d_fs_cnt);
+            r->d_fs_out = nullptr;
+            r->d_fs_cnt = nullptr;
+            r->fs_cap = 0;
+            if ((q = dalloc(&r->d_fs_out, 2 * outn))) return q;
+            if ((q = dalloc(&r->d_fs_cnt, outn))) return q;
+            r->fs_cap = outn;
+        }
+        double *const d_out = r->d_fs_out;
+        int32_t *const d_cnt = r->d_fs_cnt;
         if (n_frame) {
             HIP_TRY(hipMemcpy(d_fuv, frame_u, (size_t)n_frame * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(d_fuv + n_frame, frame_v, (size_t)n_frame * 4, hipMemcpyHostToDevice));

@@ -373,22 +373,33 @@ class FlipRun:
                                           _p(sums, ctypes.c_int64), _p(acf, ctypes.c_double)), "fc_run_autocorr")
         return sums, acf
 
-    def frame_series(self, frame, chains: Optional[Sequence[int]] = None) -> Dict[str, np.ndarray]:
+    def frame_series(self, frame, chains: Optional[Sequence[int]] = None,
+                     out: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
         """Slope / angle of the frame cut edges after every accepted flip of the window, on
         the device (``fc_run_frame_series``; ``grid_chain_sec11.py:55-78,371-394``).
 
         ``frame`` is a :class:`~flipcomplexityempirical_amd.graphs.SlopeFrame`.  Returns
         ``slope``, ``angle``, ``n_cut`` as ``[len(chains), max_events + 1]`` (entry 0: window
-        start) and ``len`` per chain; use :meth:`yield_series` for the per-yield lists."""
+        start) and ``len`` per chain; use :meth:`yield_series` for the per-yield lists.
+        ``out`` (optional): host buffers ``slope`` / ``angle`` (float64) and ``n_cut`` (int32) of
+        shape ``[>= len(chains), >= events + 1]`` to fill instead of new arrays (a caller that
+        reads many chunks keeps its pages mapped); the result then holds views of them."""
         ch = np.arange(self.n_chains) if chains is None else np.asarray(chains, dtype=np.int64)
         if ch.size == 0:
             raise ValueError("frame_series: no chains")
         c0, nc = int(ch.min()), int(ch.max() - ch.min() + 1)
         st = self.stats()
         cap = int(st["events"][c0:c0 + nc].max()) + 1
-        slope = np.zeros((nc, cap), dtype=np.float64)
-        angle = np.zeros((nc, cap), dtype=np.float64)
-        ncut = np.zeros((nc, cap), dtype=np.int32)
+        # every entry is copied from the device (entries past a chain's ``len`` are padding)
+        if out is not None and out["slope"].shape[0] * out["slope"].shape[1] >= nc * cap:
+            # the buffers' leading nc * cap entries, viewed as [nc, cap]
+            slope = out["slope"].reshape(-1)[:nc * cap].reshape(nc, cap)
+            angle = out["angle"].reshape(-1)[:nc * cap].reshape(nc, cap)
+            ncut = out["n_cut"].reshape(-1)[:nc * cap].reshape(nc, cap)
+        else:
+            slope = np.empty((nc, cap), dtype=np.float64)
+            angle = np.empty((nc, cap), dtype=np.float64)
+            ncut = np.empty((nc, cap), dtype=np.int32)
         ln = np.zeros(nc, dtype=np.int64)
         eu = np.ascontiguousarray(frame.eu, dtype=np.int32)
         ev = np.ascontiguousarray(frame.ev, dtype=np.int32)
@@ -400,6 +411,8 @@ class FlipRun:
                                               _p(ncut, ctypes.c_int32), _p(ln, ctypes.c_int64)),
               "fc_run_frame_series")
         sel = ch - c0
+        if sel.size == nc and np.array_equal(sel, np.arange(nc)):  # a contiguous range: no copies
+            return {"slope": slope, "angle": angle, "n_cut": ncut, "len": ln}
         return {"slope": slope[sel], "angle": angle[sel], "n_cut": ncut[sel], "len": ln[sel]}
 
     def yield_series(self, values: np.ndarray, chain: int = 0) -> np.ndarray:
