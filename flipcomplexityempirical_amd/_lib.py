@@ -12,6 +12,8 @@ from . import build as _build
 
 _P = ctypes.POINTER
 
+FC_ABI_VERSION = 3  # include/flipchain.h: fc_params layout version
+
 FC_OK = 0
 FC_ERR_ARG = -1
 FC_ERR_INVALID_STATE = -2
@@ -29,7 +31,7 @@ FC_CON_CONTIG, FC_CON_POP, FC_CON_BOUNDARY, FC_CON_FIXED, FC_CON_EMPTY = 0x1, 0x
 
 EXPORTED = [
     "fc_graph_create", "fc_graph_get_info", "fc_graph_edges", "fc_graph_rings", "fc_graph_destroy",
-    "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_set_initial_wait", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
+    "fc_params_init", "fc_run_create", "fc_run_steps", "fc_run_set_tape", "fc_run_set_initial_wait", "fc_run_sync", "fc_run_last_ms", "fc_run_timings",
     "fc_run_read_stats", "fc_run_read_state", "fc_run_read_pops", "fc_run_read_trace", "fc_run_read_recom_trace",
     "fc_run_trace_reset", "fc_run_read_hist", "fc_run_checkpoint", "fc_run_restore",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_flips_exact", "fc_run_read_wait_expected",
@@ -46,7 +48,7 @@ class GraphInfo(ctypes.Structure):
 
 
 class Params(ctypes.Structure):
-    _fields_ = [("k", ctypes.c_int32), ("proposal", ctypes.c_int32), ("base", ctypes.c_double),
+    _fields_ = [("struct_size", ctypes.c_uint32), ("abi_version", ctypes.c_uint32), ("k", ctypes.c_int32), ("proposal", ctypes.c_int32), ("base", ctypes.c_double),
                 ("pop_lo", ctypes.c_int64), ("pop_hi", ctypes.c_int64), ("seed", ctypes.c_uint64),
                 ("chain_id_offset", ctypes.c_uint32), ("diag_mask", ctypes.c_uint32),
                 ("flags", ctypes.c_uint32), ("device", ctypes.c_int32), ("trace_chains", ctypes.c_int32),
@@ -62,7 +64,9 @@ class Params(ctypes.Structure):
                 ("tune_par_min", ctypes.c_int32), ("tune_wait_queue", ctypes.c_int32),
                 ("tune_chains_per_block", ctypes.c_int32), ("tune_prio_div", ctypes.c_int32 * 3),
                 ("tune_prio_th", ctypes.c_float * 3), ("tune_search_waves", ctypes.c_int32),
-                ("tune_deal", ctypes.c_int32)]
+                ("tune_deal", ctypes.c_int32),
+                # per-chain configuration
+                ("chain_pop_bounds", _P(ctypes.c_int64))]
 
 
 class ChainStats(ctypes.Structure):
@@ -125,6 +129,7 @@ def load(build_if_missing: bool = True):
     L.fc_graph_rings.argtypes = [vp, _P(i32), _P(ctypes.c_uint64)]
     L.fc_graph_destroy.argtypes = [vp]
     L.fc_graph_destroy.restype = None
+    L.fc_params_init.argtypes = [_P(Params), u32]
     L.fc_run_create.argtypes = [vp, _P(Params), i32, _P(ctypes.c_int8), _P(dbl), _P(vp)]
     L.fc_run_steps.argtypes = [vp, i64, i64, vp]
     L.fc_run_set_tape.argtypes = [vp, _P(ctypes.c_uint32), i64]

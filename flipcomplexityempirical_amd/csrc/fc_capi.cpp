@@ -67,6 +67,7 @@ struct fc_run {
     int32_t *d_fs_cnt = nullptr; // ... frame-cut counts
     size_t fs_cap = 0;           // entries per output array held
     char kname[96] = {0};        // last launched flip-kernel instance
+    uint64_t param_hash = 0;     // FNV-1a of every trajectory-determining parameter (checkpoint check)
     bool variant = false;        // accept / constraint variants (FULL k = 2 instance)
     struct {                     // fc_params.tune_* with the defaults filled in
         int32_t nsub, hit_stop, par_min, wait_q, wpb, coop, deal;
@@ -113,6 +114,13 @@ void free_run(fc_run *r) {
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
+}
+
+// FNV-1a over a byte range (checkpoint parameter hash)
+uint64_t fnv1a(uint64_t h, const void *data, size_t bytes) {
+    const unsigned char *b = (const unsigned char *)data;
+    for (size_t i = 0; i < bytes; ++i) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
 }
 
 bool district_contiguous(const fc::HostGraph &g, const int8_t *a, int k, std::vector<int32_t> &q,
@@ -222,6 +230,23 @@ int fc_graph_rings(const fc_graph *g, int32_t *ring, uint64_t *meta) {
 
 void fc_graph_destroy(fc_graph *g) { delete g; }
 
+int fc_params_init(fc_params *p, uint32_t struct_size) {
+    if (!p) return fail(FC_ERR_ARG, "fc_params_init: null argument");
+    if (struct_size != sizeof(fc_params))
+        return fail(FC_ERR_ARG, "fc_params_init: struct_size " + std::to_string(struct_size) + " != sizeof(fc_params) " +
+                                    std::to_string(sizeof(fc_params)) + " (the caller's flipchain.h is another version)");
+    std::memset(p, 0, sizeof *p);
+    p->struct_size = (uint32_t)sizeof(fc_params);
+    p->abi_version = FC_ABI_VERSION;
+    p->k = 2;
+    p->base = 1.0;
+    p->pop_lo = 0;
+    p->pop_hi = INT32_MAX;
+    p->hit_lo = 1;  // hitting-time window off (hit_lo > hit_hi)
+    p->hit_hi = 0;
+    return FC_OK;
+}
+
 int32_t fc_run_n_chains(const fc_run *r) { return r ? r->n_chains : 0; }
 
 int32_t fc_run_chain_lds_bytes(const fc_run *r) { return r ? r->chain_lds_bytes : 0; }
@@ -231,6 +256,12 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     if (!out) return fail(FC_ERR_ARG, "fc_run_create: null output");
     *out = nullptr;
     if (!gr || !p || !init_assign || n_chains <= 0) return fail(FC_ERR_ARG, "fc_run_create: null argument or n_chains <= 0");
+    // the caller's fc_params layout must be this library's: nothing past struct_size is read
+    if (p->struct_size != sizeof(fc_params) || p->abi_version != FC_ABI_VERSION)
+        return fail(FC_ERR_ARG, "fc_run_create: fc_params.struct_size " + std::to_string(p->struct_size) +
+                                    " / abi_version " + std::to_string(p->abi_version) + " do not match this library (" +
+                                    std::to_string(sizeof(fc_params)) + " / " + std::to_string(FC_ABI_VERSION) +
+                                    "): set them with fc_params_init or sizeof / FC_ABI_VERSION of the same flipchain.h");
     if (p->k < 2 || p->k > fc::kMaxKGeneral)
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: k must be in [2, 32]");
     if (p->proposal == FC_PROPOSE_BI_SIGN && p->k != 2)
@@ -271,8 +302,15 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         for (int32_t i = 0; i < p->n_frozen; ++i)
             if (p->frozen[i] < 0 || p->frozen[i] >= n) return fail(FC_ERR_ARG, "fc_run_create: frozen node out of range");
     }
-    if (p->pop_lo > INT32_MAX || p->pop_hi > INT32_MAX || p->pop_lo < INT32_MIN || p->pop_hi < INT32_MIN)
-        return fail(FC_ERR_UNSUPPORTED, "fc_run_create: population bounds must fit int32");
+    // population bounds per chain (fc_params.chain_pop_bounds, else pop_lo / pop_hi for all)
+    std::vector<int64_t> pop_bounds(2 * (size_t)n_chains);
+    for (int32_t c = 0; c < n_chains; ++c) {
+        pop_bounds[2 * (size_t)c] = p->chain_pop_bounds ? p->chain_pop_bounds[2 * (size_t)c] : p->pop_lo;
+        pop_bounds[2 * (size_t)c + 1] = p->chain_pop_bounds ? p->chain_pop_bounds[2 * (size_t)c + 1] : p->pop_hi;
+        for (int j = 0; j < 2; ++j)
+            if (pop_bounds[2 * (size_t)c + j] > INT32_MAX || pop_bounds[2 * (size_t)c + j] < INT32_MIN)
+                return fail(FC_ERR_UNSUPPORTED, "fc_run_create: population bounds must fit int32");
+    }
     for (int64_t i = 0; i < (int64_t)n_chains * n; ++i)
         if (init_assign[i] < 0 || init_assign[i] >= k) return fail(FC_ERR_ARG, "fc_run_create: district id out of range");
 
@@ -292,6 +330,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     }
     r->p.log1mp = nullptr;
     r->p.frozen = nullptr;
+    r->p.chain_pop_bounds = nullptr;
     r->p.con_valid = con_valid;
     r->variant = variant;
     r->n_chains = n_chains;
@@ -408,7 +447,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         }
         if (con_valid & FC_CON_POP)
             for (int d = 0; d < k; ++d)
-                if (pops[d] < p->pop_lo || pops[d] > p->pop_hi)
+                if (pops[d] < pop_bounds[2 * (size_t)c] || pops[d] > pop_bounds[2 * (size_t)c + 1])
                     return fail(FC_ERR_INVALID_STATE, "chain " + std::to_string(c) +
                                                           ": The given initial_state is not valid according is_valid (population).");
         if ((con_valid & FC_CON_BOUNDARY) && (ng[0] == 0 || ng[1] == 0))
@@ -449,6 +488,8 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         s.ngamma[0] = ng[0];
         s.ngamma[1] = ng[1];
         s.last_flip = -1;
+        s.pop_lo = (int32_t)pop_bounds[2 * (size_t)c];
+        s.pop_hi = (int32_t)pop_bounds[2 * (size_t)c + 1];
         int64_t wait0 = 0;
         if (p->diag_mask & FC_DIAG_WAIT) {
             const uint32_t gid = p->chain_id_offset + (uint32_t)c;
@@ -491,6 +532,22 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
             else t = (uint64_t)std::ceil(bound * 9007199254740992.0);
             thresh[(size_t)c * (2 * R + 1) + (dd + R)] = t;
         }
+    }
+
+    // every parameter a trajectory depends on besides seed / chain ids, for fc_run_restore
+    {
+        uint64_t h = 0xcbf29ce484222325ull;
+        h = fnv1a(h, thresh.data(), thresh.size() * 8);
+        h = fnv1a(h, pop_bounds.data(), pop_bounds.size() * 8);
+        h = fnv1a(h, r->labels.data(), r->labels.size() * 4);
+        h = fnv1a(h, r->log1mp.data(), r->log1mp.size() * 8);
+        const int64_t scal[] = {k, p->proposal, p->accept, (int64_t)con_valid, (int64_t)p->con_accept, p->flags,
+                                r->wmax, p->hit_lo, p->hit_hi, p->recom_node_repeats, p->recom_max_attempts};
+        h = fnv1a(h, scal, sizeof scal);
+        const double dscal[] = {p->beta, p->recom_pop_target, p->recom_epsilon, bases ? bases[0] : p->base};
+        h = fnv1a(h, dscal, sizeof dscal);
+        if (p->n_frozen > 0) h = fnv1a(h, p->frozen, (size_t)p->n_frozen * 4);
+        r->param_hash = h;
     }
 
     // ---- device ---------------------------------------------------------------------------
@@ -856,11 +913,12 @@ int fc_run_timings(fc_run *r, float *ms, int32_t cap, int32_t *n) {
 namespace {
 
 struct CkptHeader {
-    char magic[8];          // "FCCKPT01"
+    char magic[8];          // "FCCKPT02"
     int32_t n_chains, n, n_edges, k, ring_max, proposal, npad, dgraph;
     uint32_t diag_mask;
-    int32_t reserved;
+    uint32_t chain_id_offset;
     int64_t ev_cap, payload;
+    uint64_t seed, param_hash;  // the random stream and every trajectory-determining parameter
 };
 
 // (device pointer, bytes) of every buffer a checkpoint carries, in blob order
@@ -901,7 +959,7 @@ static std::vector<std::pair<void *, size_t>> ckpt_sections(fc_run *r) {
 
 CkptHeader ckpt_header(const fc_run *r, int64_t payload) {
     CkptHeader h{};
-    std::memcpy(h.magic, "FCCKPT01", 8);
+    std::memcpy(h.magic, "FCCKPT02", 8);
     h.n_chains = r->n_chains;
     h.n = r->g.n;
     h.n_edges = r->g.n_edges;
@@ -913,6 +971,9 @@ CkptHeader ckpt_header(const fc_run *r, int64_t payload) {
     h.diag_mask = r->p.diag_mask;
     h.ev_cap = r->ev_cap;
     h.payload = payload;
+    h.chain_id_offset = r->p.chain_id_offset;
+    h.seed = r->p.seed;
+    h.param_hash = r->param_hash;
     return h;
 }
 
@@ -953,6 +1014,12 @@ int fc_run_restore(fc_run *r, const void *buf, int64_t len) {
         h.ring_max != want.ring_max || h.proposal != want.proposal || h.npad != want.npad || h.dgraph != want.dgraph ||
         h.diag_mask != want.diag_mask || h.ev_cap != want.ev_cap || h.payload != payload)
         return fail(FC_ERR_ARG, "fc_run_restore: the checkpoint was taken from a run with another graph or fc_params");
+    if (h.seed != want.seed || h.chain_id_offset != want.chain_id_offset)
+        return fail(FC_ERR_ARG, "fc_run_restore: the checkpoint's seed / chain_id_offset differ from this run's "
+                                "(its chains would continue on another random stream)");
+    if (h.param_hash != want.param_hash)
+        return fail(FC_ERR_ARG, "fc_run_restore: the checkpoint's bases / thresholds, population bounds, labels, "
+                                "log(1 - p) table or accept / constraint / ReCom settings differ from this run's");
     if (len != (int64_t)sizeof(CkptHeader) + payload) return fail(FC_ERR_ARG, "fc_run_restore: blob size mismatch");
     if (int rc = fc_run_sync(r)) return rc;
     const unsigned char *in = (const unsigned char *)buf;

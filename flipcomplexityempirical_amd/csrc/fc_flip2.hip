@@ -96,6 +96,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     int64_t ev_len = FULL ? scp->ev_len : 0, hit_time = FULL ? scp->hit_time : 0;
     int cut = scp->cut, nb = scp->nb;
     int pops0 = scp->pops[0], pops1 = scp->pops[1];
+    const int pop_lo = scp->pop_lo, pop_hi = scp->pop_hi;  // this chain's bounds (chain_pop_bounds)
     int ng0 = scp->ngamma[0], ng1 = scp->ngamma[1];
     int64_t wait_cur = scp->wait_cur;
     int qn = 0;  // queued accepted states (lean instance); the last one is the current state
@@ -488,7 +489,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const bool known = bd | !nz | exact | s_lin;
             const bool ok = ((av ? ng0 : ng1) > 0) ? okT : okN;
             const int pa = av ? pops1 : pops0, pb = av ? pops0 : pops1;
-            const bool popok = (pa - pv >= p.pop_lo) && (pb + pv <= p.pop_hi);
+            const bool popok = (pa - pv >= pop_lo) && (pb + pv <= pop_hi);
             bool valid = prop & known & ok & popok;
             bool acc_now = acc;
             bool inv_contig = !ok;  // reason of an invalid proposal: contiguity, else "pop"
@@ -550,8 +551,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 const int Gp = count_below(__ballot(cand0 && dg_l > 0)) - count_below(__ballot(cand0 && dg_l < 0));
                 const bool ok1 = ((av ? ng0 + Gp : ng1 - Gp) > 0) ? okT : okN;
                 const int q0 = pops0 + P, q1 = pops1 - P;
-                const bool valid1 = prop && known && ok1 && ((av ? q1 : q0) - pv >= p.pop_lo) &&
-                                    ((av ? q0 : q1) + pv <= p.pop_hi);
+                const bool valid1 = prop && known && ok1 && ((av ? q1 : q0) - pv >= pop_lo) &&
+                                    ((av ? q0 : q1) + pv <= pop_hi);
                 const bool cand1 = valid1 && acc;
                 const uint64_t MM = __ballot(prop && cand1 != cand0);
                 const uint64_t UU = __ballot(prop && !known);

@@ -76,6 +76,7 @@ struct ChainScalars {
     int32_t last_flip;
     int32_t stuck;
     int32_t ser_cut0, ser_nb0;  // |cut|, |B| at ser_t0
+    int32_t pop_lo, pop_hi;     // this chain's inclusive population bounds (fc_params.chain_pop_bounds)
 };
 
 // Kernel parameters (passed by value).
@@ -89,7 +90,7 @@ struct KParams {
     uint32_t lemire_thresh;     // 2^32 mod n
     uint32_t chain_id_offset;
     uint32_t seed_lo, seed_hi;
-    int32_t pop_lo, pop_hi;
+    int32_t pop_lo, pop_hi;     // (unused by the kernels: each chain's bounds are in ChainScalars)
     int64_t n_steps;            // steps to advance per chain in this launch
     int64_t max_draws;          // per chain per launch
     int8_t *assign;             // [n_chains * n]

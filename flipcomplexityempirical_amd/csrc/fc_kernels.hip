@@ -36,78 +36,8 @@ namespace fc {
 
 using namespace dev;
 
-// District-graph contiguity rule (k > 2; every node exact, so each ring lists every cell that
-// shares a face with its node and the outer face is one wedge of the outer nodes' rings).
-//
-// Removing v from its district A disconnects A (single_flip_contiguous [gc-0.2],
-// grid_chain_sec11.py:22,340) iff two "super-gaps" of v's ring -- the stretches between
-// consecutive A-runs that hold old neighbours, made of other districts' cells, irrelevant
-// A-corners and (outer nodes) the outer-face wedge -- are joined through the complement of
-// A: cells of districts != A under face adjacency, plus the outer face.  (=>: a complement
-// path from one super-gap to another, closed through v, is a curve that separates the A-runs
-// on its two sides; no A edge can cross it, since it runs through face interiors and the
-// outer face.  <=: the boundary cycle around a piece cut off by v passes through v, entering
-// and leaving through two super-gaps, and otherwise through the complement.)  Every district
-// is connected, so the complement's components are those of the district graph without A:
-// X - Y when some face holds cells of both (adj, kept incrementally from the per-chain pair
-// counts), X - outer face when X has an outer-face node (bit 31).  The verdict is a few
-// bitmask closures -- no search.  Exactness holds for any such graph; the oracle's BFS is
-// the reference (tests/test_district_rule.py checks the restatement, the GPU parity tests the
-// kernel, per proposal).
-template <int RMAX>
-__device__ __forceinline__ bool district_rule(const int (&adv)[RMAX], uint32_t inA, uint32_t nbr, uint32_t Ln,
-                                              bool gam, int A, const uint32_t *adj) {
-    // ring augmented with the outer wedge (position Ln) for outer nodes
-    const uint32_t Lp = Ln + (gam ? 1u : 0u);
-    const uint32_t fullp = (1u << Lp) - 1u;
-    inA &= (1u << Ln) - 1u;
-    const uint32_t rotA = ((inA << 1) | (inA >> (Lp - 1))) & fullp;
-    uint32_t st0 = inA & ~rotA;  // run starts
-    const uint32_t a2 = inA | (inA << Lp);
-    uint32_t relA = 0;           // A-runs holding an old neighbour
-    while (st0) {
-        const int s0 = __builtin_ctz(st0);
-        st0 &= st0 - 1u;
-        const int len = __builtin_ctz(~(a2 >> s0));
-        uint32_t run = ((1u << len) - 1u) << s0;
-        run = (run | (run >> Lp)) & fullp;
-        if (run & nbr) relA |= run;
-    }
-    const uint32_t gap = fullp & ~relA;
-    const uint32_t rotG = ((gap << 1) | (gap >> (Lp - 1))) & fullp;
-    uint32_t gst = gap & ~rotG;  // super-gap starts
-    const uint32_t g2 = gap | (gap << Lp);
-    const uint32_t notA = ~(1u << A);
-    uint32_t seen = 0;
-    while (gst) {
-        const int s0 = __builtin_ctz(gst);
-        gst &= gst - 1u;
-        const int len = __builtin_ctz(~(g2 >> s0));
-        uint32_t run = ((1u << len) - 1u) << s0;
-        run = (run | (run >> Lp)) & fullp & ~inA;
-        uint32_t D = 0;          // districts of the super-gap's cells (+ the outer face)
-        while (run) {
-            const int i = __builtin_ctz(run);
-            run &= run - 1u;
-            uint32_t di = 1u << 31;  // position Ln: the outer wedge
-#pragma unroll
-            for (int q = 0; q < RMAX; ++q) di = (q == i) ? (1u << adv[q]) : di;
-            D |= di;
-        }
-        if (D & seen) return false;
-        uint32_t comp = D, fr = D;  // closure in the district graph without A
-        while (fr) {
-            const int X = __builtin_ctz(fr);
-            fr &= fr - 1u;
-            const uint32_t nb = adj[X] & notA & ~comp;
-            if (nb & seen) return false;
-            comp |= nb;
-            fr |= nb;
-        }
-        seen |= comp;
-    }
-    return true;
-}
+// district_rule (the district-graph contiguity rule, k > 2): fc_ring.h, shared with the host
+// check tests/native/district_rule_lib.cpp.
 
 // KM = 2: two districts (BI_SIGN, and PAIR with k = 2, which coincide); the outer-face
 // exact rule applies.  KM = 0: k <= 32 districts, PAIR proposals, populations in LDS.  KM = 1:
@@ -201,6 +131,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     int64_t ev_len = scp->ev_len, hit_time = scp->hit_time;
     int cut = scp->cut, nb = scp->nb;
     int pops0 = scp->pops[0], pops1 = scp->pops[1];
+    const int pop_lo = scp->pop_lo, pop_hi = scp->pop_hi;  // this chain's bounds (chain_pop_bounds)
     int ng0 = scp->ngamma[0], ng1 = scp->ngamma[1];
     int64_t wait_cur = scp->wait_cur;
     int last_flip = scp->last_flip;
@@ -504,7 +435,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 pb = popk[tgt];
             }
             const bool ok = ((av ? ng0 : ng1) > 0) ? okT : okN;
-            const bool popok = (pa - pv >= p.pop_lo) && (pb + pv <= p.pop_hi);
+            const bool popok = (pa - pv >= pop_lo) && (pb + pv <= pop_hi);
             const bool valid = prop && known && ok && popok;
             // ---- one event at a time: the first acceptance or undecided slot -----------------
             const uint64_t VAL = __ballot(valid);

@@ -102,6 +102,7 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
     int64_t sum_cut = scp->sum_cut, sum_nb = scp->sum_nb, attempts_tot = scp->bfs_calls, trees_tot = scp->bfs_levels;
     int64_t trace_len = scp->trace_len;
     int cut = scp->cut, nb = scp->nb;
+    const int pop_lo = scp->pop_lo, pop_hi = scp->pop_hi;  // this chain's bounds (chain_pop_bounds)
     int stuck = 0;
     const uint32_t gid = p.chain_id_offset + (uint32_t)c;
     const bool trace_on = p.trace && c < p.trace_chains;
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
         const int cut_new = (int)wave_sum64(cc);
         const int64_t p0 = spop[child], p1 = popM - p0;
         int flags;
-        if (p0 < p.pop_lo || p0 > p.pop_hi || p1 < p.pop_lo || p1 > p.pop_hi) {
+        if (p0 < pop_lo || p0 > pop_hi || p1 < pop_lo || p1 > pop_hi) {
             ++inv_pop;
             flags = 8;
         } else {

@@ -3,18 +3,22 @@
 Chains are independent: global chain id g = offset(rank) + c, and the Philox counter holds
 g, so every chain's trajectory is independent of how many GPUs run it.  There is no
 data-path collective; at the end one all-reduce (RCCL over xGMI with backend "nccl", gloo on
-CPU) sums every statistic the reference's driver accumulates (grid_chain_sec11.py:350-419):
+CPU) sums every statistic the reference's driver accumulates (grid_chain_sec11.py:350-419),
+**per configuration**: every chain carries a group id -- its (pop, base, alignment)
+configuration of the sweep at :182-184, or any caller-given key -- and each statistic is kept
+as one row per group, because the reference writes and plots them per configuration
+(:383-384,396-400,416-419 accumulated, :410-528 written):
 
 * per-group scalars (AGG_FIELDS: proposals, steps, accepted, invalid counts, the per-yield
   sums behind rce / rbn / wait.txt);
-* the |cut| and |B| histograms over yields (E + 1 and N + 1 bins);
-* per-edge ``cut_times`` (:383-384, E entries);
-* per-node ``num_flips`` and ``part_sum`` (:396-400, N entries each);
-* per-node ``last_flipped`` (:398), reduced by MAX (the one non-additive field; it rides in
-  the same packed buffer as a second all-reduce with op MAX).
+* the |cut| and |B| histograms over yields (E + 1 and N + 1 bins), ``[n_groups, bins]``;
+* per-edge ``cut_times`` (:383-384), ``[n_groups, E]``;
+* per-node ``num_flips`` and ``part_sum`` (:396-400), ``[n_groups, N]`` each;
+* per-node ``last_flipped`` (:398), ``[n_groups, N]``, reduced by MAX (the one non-additive
+  field; a second all-reduce with op MAX).
 
-The sum fields travel as one packed int64 buffer (<= ~100 KB for sec11), so the collective is
-latency-bound whatever the link: xGMI bandwidth is irrelevant here.
+The sum fields travel as one packed int64 buffer (C2's 30 configurations: ~3 MB), so the
+collective is latency-bound whatever the link: xGMI bandwidth is irrelevant here.
 """
 from __future__ import annotations
 
@@ -73,22 +77,47 @@ SUM_ARRAYS = ("cut_hist", "nb_hist", "cut_times", "num_flips", "part_sum")
 MAX_ARRAYS = ("last_flipped",)
 
 
+def group_arrays(arr: np.ndarray, groups: np.ndarray, n_groups: int, op: str = "sum") -> np.ndarray:
+    """``[n_groups, len]``: the rows of a per-chain array ``[chains, len]`` summed (or maxed)
+    by group id; groups without chains give zero rows."""
+    a = np.asarray(arr, dtype=np.int64)
+    if a.ndim == 1:
+        a = a[None, :]
+    g = np.asarray(groups, dtype=np.int64).reshape(-1)
+    if g.size != a.shape[0]:
+        raise ValueError("one group id per chain")
+    if g.size and (g.min() < 0 or g.max() >= n_groups):
+        raise ValueError("group id out of range")
+    out = np.zeros((n_groups, a.shape[1]), dtype=np.int64)
+    if op == "sum":
+        np.add.at(out, g, a)
+    else:
+        for grp in np.unique(g):
+            out[grp] = a[g == grp].max(axis=0)
+    return out
+
+
 def local_statistics(stats: Dict[str, np.ndarray], groups: np.ndarray, n_groups: int,
                      arrays: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
-    """One rank's contribution: grouped scalar sums plus, for every per-chain array present
-    in ``arrays`` (``[chains, len]``), its sum (or max) over the rank's chains."""
+    """One rank's contribution, per group (configuration): grouped scalar sums and, for every
+    per-chain array present in ``arrays`` (``[chains, len]``), its ``[n_groups, len]`` sum (or
+    max, ``last_flipped``) over the rank's chains of each group."""
     out = {"scalars": group_aggregate(stats, groups, n_groups)}
     for name, arr in (arrays or {}).items():
-        a = np.asarray(arr, dtype=np.int64)
-        if a.ndim == 1:
-            a = a[None, :]
         if name in SUM_ARRAYS:
-            out[name] = a.sum(axis=0)
+            out[name] = group_arrays(arr, groups, n_groups, "sum")
         elif name in MAX_ARRAYS:
-            out[name] = a.max(axis=0) if a.shape[0] else np.zeros(a.shape[1], dtype=np.int64)
+            out[name] = group_arrays(arr, groups, n_groups, "max")
         else:
             raise KeyError(f"unknown statistic {name!r}")
     return out
+
+
+def sweep_groups(n_chains_total: int, n_configs: int, offset: int = 0, count: Optional[int] = None) -> np.ndarray:
+    """Group id of global chains offset .. offset + count - 1 when chain g runs configuration
+    g % n_configs (the bench's and the sweep drivers' dealing of configurations to chains)."""
+    count = n_chains_total - offset if count is None else count
+    return (np.arange(offset, offset + count) % n_configs).astype(np.int64)
 
 
 def _pack(d: Dict[str, np.ndarray], names) -> Tuple[np.ndarray, list]:
@@ -113,8 +142,9 @@ def _unpack(flat: np.ndarray, layout) -> Dict[str, np.ndarray]:
 
 def allreduce_statistics(local: Dict[str, np.ndarray], dist=None, device=None) -> Dict[str, np.ndarray]:
     """Every rank's ``local_statistics`` combined: one SUM all-reduce of the packed additive
-    fields (scalars, histograms, cut_times, num_flips, part_sum) and one MAX all-reduce of
-    last_flipped.  Every rank must pass the same set of fields with the same shapes."""
+    fields (scalars, histograms, cut_times, num_flips, part_sum; all ``[n_groups, ...]``) and
+    one MAX all-reduce of last_flipped.  Every rank must pass the same set of fields with the
+    same shapes (the same n_groups, even where it runs no chain of a group)."""
     flat_s, lay_s = _pack(local, ("scalars",) + SUM_ARRAYS)
     flat_m, lay_m = _pack(local, MAX_ARRAYS)
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
@@ -131,12 +161,19 @@ def allreduce_statistics(local: Dict[str, np.ndarray], dist=None, device=None) -
     return out
 
 
+def _checksum(a) -> int:
+    x = np.asarray(a, dtype=np.int64).reshape(-1)
+    w = np.arange(1, x.size + 1, dtype=np.int64)
+    return int((x * w).sum() & ((1 << 63) - 1))
+
+
 def checksums(red: Dict[str, np.ndarray]) -> Dict[str, int]:
     """Order-sensitive int64 checksums of the reduced fields (the N > 1 bench line's record of
     what the collective produced): sum_i (i + 1) * x_i mod 2^63 per field."""
-    out = {}
-    for name, a in red.items():
-        x = np.asarray(a, dtype=np.int64).reshape(-1)
-        w = np.arange(1, x.size + 1, dtype=np.int64)
-        out[name] = int((x * w).sum() & ((1 << 63) - 1))
-    return out
+    return {name: _checksum(a) for name, a in red.items()}
+
+
+def group_checksums(red: Dict[str, np.ndarray]) -> Dict[str, list]:
+    """Per-group checksums of every reduced field (row g of each ``[n_groups, ...]`` array):
+    what each configuration's outputs came to after the collective."""
+    return {name: [_checksum(row) for row in np.asarray(a)] for name, a in red.items()}

@@ -32,6 +32,11 @@ def _p(arr, ct):
     return arr.ctypes.data_as(_P(ct)) if arr is not None else _P(ct)()
 
 
+def _set_fields(struct, **fields):
+    for name, val in fields.items():
+        setattr(struct, name, val)
+
+
 class FlipGraph:
     """Native graph handle (``fc_graph_create``)."""
 
@@ -149,7 +154,10 @@ class FlipRun:
 
     def __init__(self, graph: FlipGraph, init_assign: np.ndarray, cfg: RunConfig,
                  bases: Optional[Sequence[float]] = None, n_chains: Optional[int] = None,
-                 log1mp: Optional[np.ndarray] = None):
+                 log1mp: Optional[np.ndarray] = None, pop_bounds: Optional[np.ndarray] = None):
+        """``pop_bounds`` (optional): ``[n_chains, 2]`` inclusive population bounds per chain
+        (``fc_params.chain_pop_bounds``), so that configurations of different tolerance share a
+        run; default ``cfg.pop_lo`` / ``cfg.pop_hi`` for every chain."""
         L = _lib.load()
         self.graph = graph
         self.cfg = cfg
@@ -167,14 +175,22 @@ class FlipRun:
         self._bases = None if bases is None else np.ascontiguousarray(bases, dtype=np.float64)
         if self._bases is not None and self._bases.shape[0] != self.n_chains:
             raise ValueError("bases must have one entry per chain")
-        prm = _lib.Params(k=cfg.k, proposal=int(cfg.proposal), base=float(cfg.base), wmax=int(cfg.wmax),
-                          pop_lo=int(cfg.pop_lo), pop_hi=int(cfg.pop_hi), seed=int(cfg.seed),
-                          chain_id_offset=int(cfg.chain_id_offset), diag_mask=int(cfg.diag_mask),
-                          flags=int(cfg.flags), device=int(cfg.device), trace_chains=int(cfg.trace_chains),
-                          trace_cap=int(cfg.trace_cap), labels=_p(self._labels, ctypes.c_int32),
-                          log1mp=_p(self._log1mp, ctypes.c_double), hit_lo=int(cfg.hit_lo),
-                          hit_hi=int(cfg.hit_hi), event_cap=int(cfg.event_cap), accept=int(cfg.accept),
-                          con_valid=int(cfg.con_valid), con_accept=int(cfg.con_accept), beta=float(cfg.beta))
+        self._pop_bounds = None
+        if pop_bounds is not None:
+            self._pop_bounds = np.ascontiguousarray(pop_bounds, dtype=np.int64).reshape(-1)
+            if self._pop_bounds.size != 2 * self.n_chains:
+                raise ValueError("pop_bounds must be [n_chains, 2]")
+        prm = _lib.Params()
+        check(L.fc_params_init(ctypes.byref(prm), ctypes.sizeof(_lib.Params)), "fc_params_init")
+        _set_fields(prm, k=cfg.k, proposal=int(cfg.proposal), base=float(cfg.base), wmax=int(cfg.wmax),
+                    pop_lo=int(cfg.pop_lo), pop_hi=int(cfg.pop_hi), seed=int(cfg.seed),
+                    chain_id_offset=int(cfg.chain_id_offset), diag_mask=int(cfg.diag_mask),
+                    flags=int(cfg.flags), device=int(cfg.device), trace_chains=int(cfg.trace_chains),
+                    trace_cap=int(cfg.trace_cap), labels=_p(self._labels, ctypes.c_int32),
+                    log1mp=_p(self._log1mp, ctypes.c_double), hit_lo=int(cfg.hit_lo),
+                    hit_hi=int(cfg.hit_hi), event_cap=int(cfg.event_cap), accept=int(cfg.accept),
+                    con_valid=int(cfg.con_valid), con_accept=int(cfg.con_accept), beta=float(cfg.beta))
+        prm.chain_pop_bounds = _p(self._pop_bounds, ctypes.c_int64)
         self._frozen = np.ascontiguousarray(list(cfg.frozen), dtype=np.int32)
         prm.frozen = _p(self._frozen, ctypes.c_int32)
         prm.n_frozen = int(self._frozen.size)
@@ -381,9 +397,12 @@ class FlipRun:
         ``frame`` is a :class:`~flipcomplexityempirical_amd.graphs.SlopeFrame`.  Returns
         ``slope``, ``angle``, ``n_cut`` as ``[len(chains), max_events + 1]`` (entry 0: window
         start) and ``len`` per chain; use :meth:`yield_series` for the per-yield lists.
-        ``out`` (optional): host buffers ``slope`` / ``angle`` (float64) and ``n_cut`` (int32) of
-        shape ``[>= len(chains), >= events + 1]`` to fill instead of new arrays (a caller that
-        reads many chunks keeps its pages mapped); the result then holds views of them."""
+        ``out`` (optional): C-contiguous host buffers ``slope`` / ``angle`` (float64) and
+        ``n_cut`` (int32) to fill instead of new arrays (a caller that reads many chunks keeps its
+        pages mapped); the result then holds views of their leading ``nc * cap`` entries.  A
+        buffer of another dtype or layout raises ``ValueError`` (the native call writes through
+        raw pointers); buffers too small for this call's ``nc * cap`` entries are not used (fresh
+        arrays are returned).  Entries past a chain's ``len`` are padding with undefined values."""
         ch = np.arange(self.n_chains) if chains is None else np.asarray(chains, dtype=np.int64)
         if ch.size == 0:
             raise ValueError("frame_series: no chains")
@@ -391,7 +410,13 @@ class FlipRun:
         st = self.stats()
         cap = int(st["events"][c0:c0 + nc].max()) + 1
         # every entry is copied from the device (entries past a chain's ``len`` are padding)
-        if out is not None and out["slope"].shape[0] * out["slope"].shape[1] >= nc * cap:
+        if out is not None:
+            for key, dt in (("slope", np.float64), ("angle", np.float64), ("n_cut", np.int32)):
+                buf = out.get(key)
+                if not isinstance(buf, np.ndarray) or buf.dtype != dt or not buf.flags.c_contiguous \
+                        or not buf.flags.writeable:
+                    raise ValueError(f"frame_series: out[{key!r}] must be a writeable C-contiguous {np.dtype(dt)} array")
+        if out is not None and min(out[key].size for key in ("slope", "angle", "n_cut")) >= nc * cap:
             # the buffers' leading nc * cap entries, viewed as [nc, cap]
             slope = out["slope"].reshape(-1)[:nc * cap].reshape(nc, cap)
             angle = out["angle"].reshape(-1)[:nc * cap].reshape(nc, cap)

@@ -37,6 +37,10 @@ extern "C" {
 #define FC_ERR_UNSUPPORTED (-4)  /* configuration outside what the kernels implement        */
 #define FC_ERR_NOMEM (-5)
 
+/* fc_params.struct_size / abi_version: a caller built against another layout of fc_params is
+ * rejected (FC_ERR_ARG) instead of read past.  Bumped whenever fc_params changes.           */
+#define FC_ABI_VERSION 3u
+
 /* fc_graph_create flags */
 #define FC_GRAPH_NO_EXACT 0x1u   /* never trust the planar local contiguity rule            */
 
@@ -96,11 +100,14 @@ typedef struct fc_graph_info {
 } fc_graph_info;
 
 typedef struct fc_params {
+    uint32_t struct_size;      /* sizeof(fc_params) as the caller compiled it (fc_params_init) */
+    uint32_t abi_version;      /* FC_ABI_VERSION as the caller compiled it                  */
     int32_t k;                 /* districts: 2 (BI_SIGN or PAIR) or 3..32 (PAIR)            */
     int32_t proposal;          /* FC_PROPOSE_*                                              */
     double base;               /* cut_accept base when `bases` is NULL (:171-179, :279-280) */
     int64_t pop_lo, pop_hi;    /* inclusive integer bounds equivalent to
-                                  within_percent_of_ideal_population (:319)                 */
+                                  within_percent_of_ideal_population (:319); every chain's
+                                  unless chain_pop_bounds is given                          */
     uint64_t seed;             /* Philox key (DESIGN.md "Random stream")                    */
     uint32_t chain_id_offset;  /* global id of local chain 0 (multi-GPU sharding)           */
     uint32_t diag_mask;        /* FC_DIAG_*                                                 */
@@ -131,8 +138,9 @@ typedef struct fc_params {
     /* Launch tuning.  Scheduling only: no trajectory, statistic or trace depends on these
      * (tests/test_parity_gpu.py::test_sec11_batch_shapes, test_pair_gpu.py::test_k4_wait_queue_lengths). 0 = the default;
      * the library reads no environment variables.                                          */
-    int32_t tune_nsub;          /* draw rounds of 64 per batch: k = 2 in {1, 2, 4} (default 4),
-                                   k > 2 in {1, 2} (default 1); anything else FC_ERR_ARG       */
+    int32_t tune_nsub;          /* draw rounds of 64 per batch, in {1, 2, 4}: k = 2 default 4;
+                                   k > 2 default 2 (4 when the slot bound wmax exceeds 8);
+                                   anything else FC_ERR_ARG                                    */
     int32_t tune_hit_stop;      /* no further draw round once a batch holds this many boundary
                                    hits (default 32)                                           */
     int32_t tune_par_min;       /* k = 2: segment-parallel commit from this many acceptances on
@@ -155,7 +163,17 @@ typedef struct fc_params {
                                    of the previous launch's draws (most first) instead of the
                                    dispatcher's order; 1 = on, -1 = off (default).  Changes
                                    which wave runs which chain, never a trajectory              */
+    /* Per-chain configuration.  The reference sweeps population tolerance x base x alignment
+     * (grid_chain_sec11.py:182-184); with per-chain bases (fc_run_create `bases`) and bounds the
+     * whole sweep is one run.                                                                   */
+    const int64_t *chain_pop_bounds; /* [2 * n_chains]: chain c's inclusive (pop_lo, pop_hi), or
+                                        NULL for pop_lo / pop_hi                                 */
 } fc_params;
+
+/* Zero *p, then set struct_size / abi_version and the defaults a zeroed struct does not give:
+ * base 1, pop bounds [0, INT32_MAX], hitting-time window off.  FC_ERR_ARG when struct_size is
+ * not this library's sizeof(fc_params) (the caller's header is another version).            */
+int fc_params_init(fc_params *p, uint32_t struct_size);
 
 /* Per-chain statistics.  "Yields" are the states a `for part in exp_chain` loop sees:
  * the initial state plus one per valid step; every sum runs over all yields. */
@@ -234,7 +252,9 @@ void fc_graph_destroy(fc_graph *g);
 /* ---- run: replaces Partition(graph, assignment, updaters) + MarkovChain(...) --------- */
 /* init_assign: [n_chains * n] district ids 0..k-1 (one initial plan per chain).
  * bases: [n_chains] per-chain cut_accept base, or NULL for params->base.
- * Validates every initial state like MarkovChain.__init__ (FC_ERR_INVALID_STATE). */
+ * Validates every initial state like MarkovChain.__init__ (FC_ERR_INVALID_STATE) against its
+ * chain's population bounds.  FC_ERR_ARG when p->struct_size != sizeof(fc_params) or
+ * p->abi_version != FC_ABI_VERSION (a caller compiled against another fc_params layout). */
 int fc_run_create(const fc_graph *g, const fc_params *p, int32_t n_chains, const int8_t *init_assign,
                   const double *bases, fc_run **out);
 /* Advance every chain by n_steps valid steps (the reference's step semantics: invalid
@@ -303,7 +323,8 @@ int fc_run_autocorr(fc_run *r, const int32_t *lags, int32_t nlags, int64_t *lag_
  *   mid_xy [2 n_frame]:          their midpoints (enda / endb) in the reference's node
  *                               coordinates; (cx, cy) the angle centre ((20, 20) there).
  * Output [i * cap + j] for chain c0 + i: j = 0 the window start yield, j >= 1 the state
- * created by event j - 1 (it holds for yields event.t .. next event.t - 1):
+ * created by event j - 1 (it holds for yields event.t .. next event.t - 1); entries j >= len[i]
+ * are padding and left undefined (the outputs are copied whole from a device buffer):
  *   slope (+inf when the two midpoints share x), angle = arccos(clip(cos)), n_cut = frame
  *   cut edges (< 2: slope = angle = NaN, where the reference raises IndexError).
  * len[i] = events + 1.  FC_ERR_ARG when cap is too small or a log overflowed event_cap. */
@@ -317,8 +338,10 @@ int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, cons
  * window and event log) -- as one byte blob.  fc_run_checkpoint with buf == NULL (or cap too
  * small) stores the size in *len (FC_ERR_ARG when cap is too small).  fc_run_restore loads it
  * into a run created with the same graph and fc_params (n_chains, k, proposal, diag_mask,
- * event_cap are checked; FC_ERR_ARG otherwise); the chains then continue bit for bit as if
- * never interrupted.  Per-proposal traces are outputs: they restart empty after a restore. */
+ * event_cap, seed, chain_id_offset and a hash of every trajectory-determining parameter --
+ * per-chain bases / thresholds and population bounds, labels, the log(1 - p) table, accept /
+ * constraint settings, frozen nodes, ReCom settings -- are checked; FC_ERR_ARG otherwise); the
+ * chains then continue bit for bit as if never interrupted.  Per-proposal traces are outputs: they restart empty after a restore. */
 int fc_run_checkpoint(fc_run *r, void *buf, int64_t cap, int64_t *len);
 int fc_run_restore(fc_run *r, const void *buf, int64_t len);
 /* Name of the last launched flip-kernel instance, as rocprofv3 spells it. */

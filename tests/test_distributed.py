@@ -113,10 +113,13 @@ def _real_worker(rank, world, port, q):
 
 
 def test_allreduce_all_statistics_world2_gloo():
-    """the one reduction carries the |cut| / |B| histograms, per-edge cut_times,
-    per-node num_flips / part_sum (sums) and last_flipped (max) besides the grouped scalars.
-    Real per-chain arrays from the C oracle (C1 lattice, 12 chains over 4 bases) sharded over a
-    gloo world of 2 must reduce to the host-side combination of all 12 chains."""
+    """SURVEY §8(e), per configuration: the one reduction carries the |cut| / |B| histograms,
+    per-edge cut_times, per-node num_flips / part_sum (sums) and last_flipped (max) besides the
+    grouped scalars, each as one row per group (here the base: chain g runs base g % 4, so every
+    group has chains on both ranks).  Real per-chain arrays from the C oracle (C1 lattice, 12
+    chains) sharded over a gloo world of 2 must reduce to the host-side combination of each
+    group's chains -- the reference's per-configuration outputs (grid_chain_sec11.py:383-384,
+    396-400,416-419), not their sum over configurations."""
     from oracle import flipref
     flipref.build_lib()
     ctx = mp.get_context("spawn")
@@ -132,11 +135,31 @@ def test_allreduce_all_statistics_world2_gloo():
     expect = _real_local(np.arange(N_REAL))   # every chain on one host, no collective
     assert set(expect) == {"scalars"} | set(D.SUM_ARRAYS) | set(D.MAX_ARRAYS)
     rs = [_real_chain(g) for g in range(N_REAL)]
-    assert np.array_equal(expect["cut_times"], sum(r["cut_times"] for r in rs))
-    assert np.array_equal(expect["last_flipped"], np.max([r["last_flipped"] for r in rs], axis=0))
-    # every yield (the initial state + one per step) lands in one |cut| bin
-    assert int(expect["cut_hist"].sum()) == N_REAL * (STEPS_REAL + 1)
+    ng = len(BASES_REAL)
+    for grp in range(ng):
+        members = [r for g, r in enumerate(rs) if g % ng == grp]
+        for name in D.SUM_ARRAYS:
+            assert np.array_equal(expect[name][grp], sum(r[name] for r in members)), (name, grp)
+        assert np.array_equal(expect["last_flipped"][grp], np.max([r["last_flipped"] for r in members], axis=0))
+        # every yield of the group's chains (the initial state + one per step) lands in one |cut| bin
+        assert int(expect["cut_hist"][grp].sum()) == len(members) * (STEPS_REAL + 1)
     for _, red, cs in res:
         for name, arr in expect.items():
             assert np.array_equal(red[name], arr), name
         assert cs == D.checksums(expect)
+
+
+def test_group_arrays_edge_cases():
+    a = np.arange(12, dtype=np.int64).reshape(4, 3)
+    g = np.array([2, 0, 2, 0])
+    s = D.group_arrays(a, g, 4, "sum")
+    assert s.tolist() == [[12, 14, 16], [0, 0, 0], [6, 8, 10], [0, 0, 0]]
+    m = D.group_arrays(a, g, 4, "max")
+    assert m.tolist() == [[9, 10, 11], [0, 0, 0], [6, 7, 8], [0, 0, 0]]
+    with pytest.raises(ValueError):
+        D.group_arrays(a, np.array([0, 1, 2, 4]), 4)
+    with pytest.raises(ValueError):
+        D.group_arrays(a, np.array([0, 1]), 4)
+    assert D.sweep_groups(10, 3, offset=4, count=4).tolist() == [1, 2, 0, 1]
+    cs = D.group_checksums({"x": s})
+    assert cs["x"][1] == 0 and cs["x"][0] == D.checksums({"x": s[0]})["x"]

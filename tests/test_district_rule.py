@@ -4,6 +4,11 @@ restated in Python and checked against the oracle's BFS restatement of
 chain states of the k > 2 workloads (C3 sec11 k = 4, C4 triangular k = 8, C5 Delaunay k = 6 / 18,
 FRANK k = 3) and of enclave states -- a district wholly inside another, where removing a node
 between two A-runs can leave A connected around the enclave.  CPU only."""
+import ctypes
+import os
+import shutil
+import subprocess
+
 import numpy as np
 import pytest
 
@@ -84,10 +89,46 @@ def district_rule(ring, meta, a, v, adj):
     return True, True
 
 
-def _check_states(cref, spec, states):
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(os.path.dirname(HERE), "flipcomplexityempirical_amd", "csrc")
+_KLIB = {}
+
+
+def _kernel_rule_lib(tmp_dir):
+    """csrc/fc_ring.h's district_rule -- the function flip_kernel calls -- built for the host."""
+    if "lib" not in _KLIB:
+        if shutil.which("g++") is None:
+            pytest.skip("no host C++ toolchain")
+        so = os.path.join(str(tmp_dir), "district_rule_lib.so")
+        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I", CSRC, "-o", so,
+                        os.path.join(HERE, "native", "district_rule_lib.cpp")], check=True)
+        lib = ctypes.CDLL(so)
+        i32, u32 = ctypes.c_int32, ctypes.c_uint32
+        lib.fc_test_district_rule.argtypes = [i32, ctypes.POINTER(i32), u32, u32, u32, i32, i32, ctypes.POINTER(u32)]
+        lib.fc_test_district_rule.restype = ctypes.c_int
+        _KLIB["lib"] = lib
+    return _KLIB["lib"]
+
+
+def kernel_rule(lib, ring, meta, a, v, adj):
+    """The kernel's verdict for a flip of v whose old-district neighbours are not one run:
+    district_rule(adv, inA, nbr, Ln, gam, A, adj) with the kernel's own inputs (ring cells'
+    districts, padded entries = v itself; adj words as the kernel keeps them)."""
+    R = ring.shape[1]
+    m = int(meta[v])
+    L, nbr, gam = m & 0xff, (m >> 16) & 0xffff, (m >> 9) & 1
+    adv = np.ascontiguousarray(a[ring[v]].astype(np.int32))
+    A = int(a[v])
+    inA = int(sum(1 << j for j in range(L) if adv[j] == A))
+    adjw = np.ascontiguousarray((adj & 0xffffffff).astype(np.uint32))
+    return lib.fc_test_district_rule(R, adv.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), inA, nbr, L, gam, A,
+                                     adjw.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))) == 1
+
+
+def _check_states(cref, spec, states, lib=None):
     ring, meta = FlipGraph(spec).rings()
     e = spec.edges()
-    tally = {"multi_valid": 0, "multi_invalid": 0, "checked": 0}
+    tally = {"multi_valid": 0, "multi_invalid": 0, "checked": 0, "outer_multi_valid": 0}
     for a in states:
         adj = face_adjacency(ring, meta, a)
         bn = np.unique(e[a[e[:, 0]] != a[e[:, 1]]].reshape(-1))
@@ -95,9 +136,17 @@ def _check_states(cref, spec, states):
             got, multi = district_rule(ring, meta, a, int(v), adj)
             ref = cref.flip_contiguous(spec, a, int(v)) == 1
             assert got == ref, (int(v), spec.nodes[int(v)], got, ref)
+            m = int(meta[v])
+            has_old = any(((m >> 16) >> j) & 1 and a[ring[v][j]] == a[v] for j in range(m & 0xff))
+            if lib is not None and has_old:
+                # every flip with an old-district neighbour (the kernel calls the rule off one-run rings)
+                kr = kernel_rule(lib, ring, meta, a, int(v), adj)
+                assert kr == ref, ("kernel district_rule", int(v), spec.nodes[int(v)], kr, ref)
             tally["checked"] += 1
             if multi:
                 tally["multi_valid" if got else "multi_invalid"] += 1
+                if got and (int(meta[v]) >> 9) & 1:
+                    tally["outer_multi_valid"] += 1
     return tally
 
 
@@ -112,7 +161,7 @@ def _chain_states(cref, spec, a0, k, base, pct, steps_list, seed):
 
 
 @pytest.mark.parametrize("name", ["sec11_k4", "tri_k8", "delaunay_k6", "delaunay_k18", "frank_k3"])
-def test_district_rule_equals_bfs_on_workload_states(cref, name):
+def test_district_rule_equals_bfs_on_workload_states(cref, name, tmp_path):
     if name == "sec11_k4":
         spec = G.sec11_graph()
         k, a0, base, pct = 4, None, 0.5, 0.05
@@ -131,24 +180,38 @@ def test_district_rule_equals_bfs_on_workload_states(cref, name):
         k, base, pct = 3, 0.5, 0.5
         a0 = spec.assignment_array({n: (0 if n[0] < 7 else 1 if n[0] < 14 else 2) for n in spec.nodes}, [0, 1, 2])
     states = _chain_states(cref, spec, a0, k, base, pct, [3000, 12000, 30000], seed=17)
-    t = _check_states(cref, spec, states)
+    t = _check_states(cref, spec, states, lib=_kernel_rule_lib(tmp_path))
     assert t["checked"] > 1000 and t["multi_invalid"] > 0
 
 
-def test_district_rule_enclaves(cref):
+ENCLAVES = ((7, 6), (7, 0), (7, 13), (12, 6), (13, 13), (7, 1), (1, 7), (12, 12))
+
+
+def enclave_plan(spec, ex, ey):
+    """k = 3 on a grid: district 2 a 3 x 3 block at (ex, ey) inside district 1 (x >= 6),
+    district 0 the columns x < 6."""
+    plan = {}
+    for n in spec.nodes:
+        x, y = n
+        plan[n] = 2 if (ex <= x <= ex + 2 and ey <= y <= ey + 2) else (0 if x < 6 else 1)
+    return spec.assignment_array(plan, [0, 1, 2])
+
+
+def test_district_rule_enclaves(cref, tmp_path):
     """k = 3 on a 16 x 16 grid: district 2 starts as a 3 x 3 enclave inside district 1 (it
     touches neither district 0 nor the outer face), one column of district 1 away from
     district 0.  Nodes of that column between the enclave and district 0 have two A-runs whose
     gaps are not joined in the complement -- valid multi-run flips the old same-district rule
-    could not decide; nearby enclave placements and short chains from them add more."""
+    could not decide; nearby enclave placements and short chains from them add more.  Enclaves
+    one row or column from the outer face ((7, 1), (1, 7)) make outer nodes whose ring's A-runs
+    are separated by the enclave and the outer-face wedge: valid flips, which the kernel's rule
+    used to reject (the wedge took district A's bit on rings shorter than RMAX).
+    Both the restatement and the kernel's own district_rule, built for the host, must equal
+    the BFS."""
     spec = G.grid_graph(16, 16)
     states = []
-    for ex, ey in ((7, 6), (7, 0), (7, 13), (12, 6), (13, 13)):
-        plan = {}
-        for n in spec.nodes:
-            x, y = n
-            plan[n] = 2 if (ex <= x <= ex + 2 and ey <= y <= ey + 2) else (0 if x < 6 else 1)
-        a0 = spec.assignment_array(plan, [0, 1, 2])
+    for ex, ey in ENCLAVES:
+        a0 = enclave_plan(spec, ex, ey)
         states += [a0] + _chain_states(cref, spec, a0, 3, 4.0, 0.9, [5, 30, 200], seed=5 + ex + ey)
-    t = _check_states(cref, spec, states)
-    assert t["multi_valid"] > 0 and t["multi_invalid"] > 0, t
+    t = _check_states(cref, spec, states, lib=_kernel_rule_lib(tmp_path))
+    assert t["multi_valid"] > 0 and t["multi_invalid"] > 0 and t["outer_multi_valid"] > 0, t

@@ -266,3 +266,22 @@ def test_instance_selection_and_agreement(gpu, sec11):
     for key in ("steps", "proposals", "accepted", "sum_cut", "sum_nb", "sum_wait", "cut", "nb"):
         assert np.array_equal(r2[0].stats()[key], r2[1].stats()[key]), key
     assert np.array_equal(r2[0].state(), r2[1].state())
+
+
+@pytest.mark.parametrize("flags", [0, _lib.FC_FLAG_FORCE_BFS])
+def test_enclave_states_district_rule(gpu, cref, flags):
+    """k = 3 grids whose district 2 starts as an enclave inside district 1, some of them one row
+    or column from the outer face (tests/test_district_rule.py ENCLAVES): outer nodes there have
+    their old-district neighbours on two ring runs separated by the enclave and the outer-face
+    wedge, and flipping them keeps district 1 connected around the enclave.  The district-graph
+    instance (KM = 3) rejected exactly those flips before the wedge fix; it and the
+    forced-search instance must match the oracle's BFS per proposal."""
+    from test_district_rule import ENCLAVES, enclave_plan
+    spec = G.grid_graph(16, 16)
+    k = 3
+    inits = np.stack([enclave_plan(spec, ex, ey) for ex, ey in ENCLAVES] * 2)
+    bases = np.asarray([4.0] * len(ENCLAVES) + [1.0] * len(ENCLAVES))
+    run = _run_pair(spec, inits, bases, k, steps=600, pct=0.95, flags=flags)
+    want = "fc::flip_kernel<8, 2, 0, " if flags else "fc::flip_kernel<8, 2, 3, "
+    assert run.kernel_name().startswith(want), run.kernel_name()
+    _check(cref, spec, run, k, inits, bases, steps=600, pct=0.95)

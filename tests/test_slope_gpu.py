@@ -114,3 +114,27 @@ def test_kernel_name_reported(gpu):
     run = FlipRun(fg, a0[None, :], RunConfig(seed=1, pop_lo=lo, pop_hi=hi))
     run.steps(10)
     assert run.kernel_name().startswith("fc::flip2_kernel<8, ")
+
+
+def test_frame_series_out_buffers_checked(gpu, sec11):
+    """Caller-supplied host buffers: the native call writes nc * cap entries through
+    raw pointers, so a buffer of another dtype or a non-contiguous one is refused; buffers that
+    are large enough and well-formed are filled in place, too-small ones are not used."""
+    run, _ = _run(sec11, [G.sec11_plan(0, sec11.nodes)] * 4, [G.SEC11_MU] * 4, 0.1)
+    run.steps(300)
+    frame = G.slope_frame(sec11, "sec11")
+    ref = run.frame_series(frame)
+    n = 4 * (int(run.stats()["events"].max()) + 1)
+    good = {"slope": np.empty(n), "angle": np.empty(n), "n_cut": np.empty(n, dtype=np.int32)}
+    got = run.frame_series(frame, out=good)
+    assert np.shares_memory(got["slope"], good["slope"])
+    for key in ("slope", "angle", "n_cut"):
+        live = np.arange(got[key].shape[1])[None, :] < got["len"][:, None]
+        assert np.array_equal(got[key][live], ref[key][live], equal_nan=key != "n_cut")
+    for key, bad in (("n_cut", np.empty(n, dtype=np.int64)), ("angle", np.empty(n, dtype=np.float32)),
+                     ("slope", np.empty(2 * n)[::2])):
+        with pytest.raises(ValueError, match=key):
+            run.frame_series(frame, out={**good, key: bad})
+    small = {k: v[:1] for k, v in good.items()}
+    got2 = run.frame_series(frame, out=small)
+    assert not np.shares_memory(got2["slope"], good["slope"])
