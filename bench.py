@@ -496,7 +496,7 @@ def main():
                     if c4diag else None,
                     "reduced": {"ranks": world, "collectives": "allreduce SUM (scalars, histograms, cut_times, "
                                 "num_flips, part_sum) + allreduce MAX (last_flipped), one row per configuration",
-                                "groups": W.n_groups, "group_of_chain": "g % %d" % W.n_groups,
+                                "groups": W.n_groups, "group_of_chain": f"g % {W.n_groups}",
                                 "yields": yields, "cut_hist_mass": int(red["cut_hist"].sum()) if "cut_hist" in red else None,
                                 "cut_hist_mass_per_group_ok": (bool(np.array_equal(
                                     red["cut_hist"].sum(axis=1),

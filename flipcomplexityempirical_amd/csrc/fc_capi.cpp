@@ -47,6 +47,7 @@ struct fc_run {
     int64_t *d_num_flips = nullptr, *d_part_sum = nullptr, *d_last_flipped = nullptr;
     int64_t *d_flip_count = nullptr, *d_occ_acc = nullptr, *d_last_accept = nullptr;  // FC_DIAG_FLIPS_EXACT
     int32_t *d_popk = nullptr;
+    int32_t *d_nfh = nullptr;   // k > 2: per chain, nodes per foreign-district count (PAIR slot bound)
     int32_t *d_mcnt = nullptr, *d_ngk = nullptr;  // k > 2 district-graph rule tables
     bool dgraph = false;
     int32_t wmax = 1;
@@ -107,7 +108,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh,
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_nfh, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh,
                     r->d_fs_out, r->d_fs_cnt};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -353,9 +354,14 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     if (!recom && k > 2)  // fc_kernels.hip: a, fcnt, thresholds, [BFS scratch | district tables], slots,
                           // district populations, wait queue
         r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + (r->dgraph ? fc::dgraph_lds_bytes(k) : fc::bfs_bytes(n)) +
-                             5 * 64 * 4 + fc::kMaxKGeneral * 4 + fc::kWaitQK * 16;
+                             5 * 64 * 4 + fc::kMaxKGeneral * 4 + fc::kNfh * 4 + fc::kWaitQK * 16;
+    // PAIR slot bound: fc_params.wmax > 0 fixes it; otherwise the canonical stream's bound is
+    // the state's largest foreign-district count (kept on the device, r->wmax = 0)
     r->wmax = 1;
-    if (k > 2) r->wmax = p->wmax > 0 ? p->wmax : std::max(1, std::min(g.max_degree, k - 1));
+    if (k > 2) r->wmax = p->wmax > 0 ? p->wmax : 0;
+    if (k > 2 && p->wmax > 0 && p->wmax < std::min(g.max_degree, k - 1))  // would skew the proposal
+        return fail(FC_ERR_ARG, "fc_run_create: a fixed PAIR slot bound (wmax) must be >= min(max degree, k - 1) = " +
+                                    std::to_string(std::min(g.max_degree, k - 1)) + " (<= 0: the canonical dynamic bound)");
 #ifdef FC_PHASE_PROF
     r->chain_lds_bytes += fc::kProfSlots * 8;  // phase-cycle accumulators (diagnostic build)
 #endif
@@ -425,6 +431,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     std::vector<uint8_t> fcnt((size_t)n_chains * r->npad, 0);
     std::vector<fc::ChainScalars> sc(n_chains);
     std::vector<int32_t> popk((size_t)n_chains * fc::kMaxKGeneral, 0);
+    std::vector<int32_t> nfh(k > 2 && !recom ? (size_t)n_chains * fc::kNfh : 0, 0);
     std::vector<int32_t> mcnt(r->dgraph ? (size_t)n_chains * k * k : 0, 0), ngk(r->dgraph ? (size_t)n_chains * 32 : 0, 0);
     std::vector<uint64_t> thresh((size_t)n_chains * (2 * R + 1));
     std::vector<int32_t> q;
@@ -459,8 +466,17 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         int32_t cut = 0, nb = 0;
         for (int32_t e = 0; e < E; ++e) cut += a[g.eu[e]] != a[g.ev[e]];
         for (int32_t u = 0; u < n; ++u) {
+            // k = 2: foreign neighbours; k > 2: foreign districts nf(u) (the PAIR slot count)
             int32_t f = 0;
-            for (int32_t j = g.row_ptr[u]; j < g.row_ptr[u + 1]; ++j) f += a[g.col_idx[j]] != a[u];
+            uint32_t dm = 0;
+            for (int32_t j = g.row_ptr[u]; j < g.row_ptr[u + 1]; ++j) {
+                f += a[g.col_idx[j]] != a[u];
+                if (a[g.col_idx[j]] != a[u]) dm |= 1u << a[g.col_idx[j]];
+            }
+            if (k > 2 && !recom) {
+                f = __builtin_popcount(dm);
+                nfh[(size_t)c * fc::kNfh + f] += 1;
+            }
             fcnt[(size_t)c * r->npad + u] = (uint8_t)f;
             nb += f > 0;
         }
@@ -573,6 +589,10 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     HIP_TRY(hipMemcpy(r->d_fcnt, fcnt.data(), fcnt.size(), hipMemcpyHostToDevice));
     if ((rc = dalloc(&r->d_popk, popk.size()))) return rc;
     HIP_TRY(hipMemcpy(r->d_popk, popk.data(), popk.size() * 4, hipMemcpyHostToDevice));
+    if (!nfh.empty()) {
+        if ((rc = dalloc(&r->d_nfh, nfh.size()))) return rc;
+        HIP_TRY(hipMemcpy(r->d_nfh, nfh.data(), nfh.size() * 4, hipMemcpyHostToDevice));
+    }
     if (r->dgraph) {
         if ((rc = dalloc(&r->d_mcnt, mcnt.size()))) return rc;
         HIP_TRY(hipMemcpy(r->d_mcnt, mcnt.data(), mcnt.size() * 4, hipMemcpyHostToDevice));
@@ -700,8 +720,9 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.dgraph = r->dgraph ? 1 : 0;
     k.mcnt = r->d_mcnt;
     k.ngk = r->d_ngk;
-    k.wmax = r->wmax;
-    k.wthresh = (uint32_t)((1ull << 32) % (uint64_t)r->wmax);
+    k.wmax = r->wmax > 0 ? r->wmax : 1;
+    k.wdyn = r->p.k > 2 && r->wmax <= 0 ? 1 : 0;
+    k.nfh = r->d_nfh;
     k.chain_lds_bytes = r->chain_lds_bytes;
     k.words = r->words;
     k.lab_words = fc::bfs_lab_words(r->g.n);
@@ -931,6 +952,7 @@ static std::vector<std::pair<void *, size_t>> ckpt_sections(fc_run *r) {
     if (r->p.proposal != FC_PROPOSE_RECOM) {
         v.emplace_back(r->d_fcnt, C * r->npad);
         v.emplace_back(r->d_popk, C * fc::kMaxKGeneral * 4);
+        if (r->d_nfh) v.emplace_back(r->d_nfh, C * fc::kNfh * 4);
         v.emplace_back(r->d_thresh, C * (2 * R + 1) * 8);
         if (r->dgraph) {
             v.emplace_back(r->d_mcnt, C * k * k * 4);

@@ -117,8 +117,9 @@ struct KParams {
     const uint32_t *tape;       // replay tape or null
     int64_t tape_draws;
     int32_t *popk;              // [n_chains * 32] district populations (k > 2)
-    int32_t wmax;               // PAIR: foreign-district slots per node draw
-    uint32_t wthresh;           // 2^32 mod wmax
+    int32_t wmax;               // PAIR: fixed slot bound per node draw (wdyn == 0)
+    int32_t wdyn;               // PAIR: slot bound = the state's largest foreign-district count
+    int32_t *nfh;               // [n_chains * kNfh] PAIR: nodes per foreign-district count
     fc_event *events;           // [n_chains * ev_cap] (FC_DIAG_SERIES)
     int64_t ev_cap;
     int32_t hit_lo, hit_hi;     // hitting-time window on |cut| (lo > hi: off)
@@ -166,6 +167,8 @@ constexpr int kProfSlots = 24;
 constexpr int kWaitQ = 64;
 // k > 2 kernel: 32 entries, so that sec11 chains keep four waves per SIMD in 160 KB of LDS
 constexpr int kWaitQK = 32;
+// k > 2 kernel: histogram bins of the per-node foreign-district counts (0..31)
+constexpr int kNfh = 32;
 
 // ReCom kernel parameters (fc_recom.hip).
 struct RecomParams {

@@ -79,9 +79,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     // never runs and its scratch is not allocated (fc_run_create)
     uint32_t *slot = KM != 2 && p.dgraph ? (uint32_t *)(T + (2 * RMAX + 2)) : (uint32_t *)(bs.nxt + p.words);
     int32_t *popk = (int32_t *)(slot + 5 * 64);    // [32] district populations (KM = 0)
+    // PAIR slot bound: fcnt[u] holds nf(u), u's number of foreign districts (its pairs in
+    // b_nodes, :151-153), and nfh[j] the nodes with nf = j; the canonical stream draws slots
+    // r < wcap = max_u nf(u) (p.wdyn), else r < p.wmax
+    int32_t *nfh = popk + kMaxKGeneral;
     // accepted states whose geometric wait is still to be drawn (kWaitQK: creating draw, |B|
     // after the flip, yields so far); as in fc_flip2.hip, drained by wait_flush
-    uint64_t *q_d = (uint64_t *)(popk + kMaxKGeneral);
+    uint64_t *q_d = (uint64_t *)(nfh + kNfh);
     uint32_t *q_nb = (uint32_t *)(q_d + kWaitQK), *q_run = q_nb + kWaitQK;
     // district-graph rule (p.dgraph): pair counts [k * k], adjacency masks [32] (entry 31: the
     // outer face), outer-face nodes per district [32]
@@ -106,7 +110,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             ((uint4 *)fcnt)[i] = gf[i];
         }
         if (lane < 2 * RMAX + 1) T[lane] = p.thresh[(size_t)c * (2 * RMAX + 1) + lane];
-        if (KM != 2 && lane < 32) popk[lane] = p.popk[(size_t)c * 32 + lane];
+        if (KM != 2 && lane < 32) {
+            popk[lane] = p.popk[(size_t)c * 32 + lane];
+            nfh[lane] = p.nfh[(size_t)c * kNfh + lane];
+        }
         if (dgraph) {
             const int kk = p.k * p.k;
             for (int i = lane; i < kk; i += kWave) mcnt[i] = p.mcnt[(size_t)c * kk + i];
@@ -123,6 +130,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             if (lane < 32) adj[lane] = lane == 31 ? om : m;
         }
     }
+    // slot bound of the PAIR draws and its Lemire threshold 2^32 mod wcap (wave-uniform)
+    int wcap = p.wmax;
+    if (KM != 2 && p.wdyn) {
+        wave_sync();
+        const uint64_t hm = __ballot(lane >= 1 && lane < kNfh && nfh[lane] > 0);
+        wcap = hm ? 63 - __builtin_clzll(hm) : 1;
+    }
+    uint32_t wthr = (0u - (uint32_t)wcap) % (uint32_t)wcap;
     ChainScalars *scp = p.sc + c;
     uint64_t draw = scp->draw;
     int64_t steps = scp->steps;  // index of the current yield
@@ -208,8 +223,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 // foreign district if r < fcnt[v] (foreign neighbours >= foreign districts):
                 // slots beyond are non-proposals whatever 1b would find, so they take no slot
                 // (a slot rejected by the Lemire map never proposes: not a non-hit either)
-                const uint64_t mw = (uint64_t)w.x3 * (uint64_t)(uint32_t)p.wmax;
-                ok = ok && (uint32_t)mw >= p.wthresh;
+                const uint64_t mw = (uint64_t)w.x3 * (uint64_t)(uint32_t)wcap;
+                ok = ok && (uint32_t)mw >= wthr;
                 hit = ok && (int)(mw >> 32) < (int)fcnt[v];
             } else {
                 hit = ok && fcnt[v] != 0;
@@ -259,6 +274,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         int tgt;             // target district
         bool slot_ok = true;
         int adv[RMAX];       // districts of the ring cells (KM = 0)
+        int nf_after = 0;    // KM != 2: foreign districts of v after its flip
         if constexpr (KM == 2) {
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) inA |= (uint32_t)(a[ring_entry<RMAX>(rec.ring, i)] == av) << i;
@@ -266,22 +282,24 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             tgt = 1 - av;                       // -1 * assignment, grid_chain_sec11.py:145
             tmask = nbr & ~inA;
         } else {
-            uint32_t dm = 0;                    // foreign districts among the neighbours
+            uint32_t dall = 0;                  // districts among the neighbours
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) {
                 adv[i] = a[ring_entry<RMAX>(rec.ring, i)];
                 inA |= (uint32_t)(adv[i] == av) << i;
-                if (((nbr >> i) & 1u) && adv[i] != av) dm |= 1u << adv[i];
+                if ((nbr >> i) & 1u) dall |= 1u << adv[i];
             }
+            const uint32_t dm = dall & ~(1u << av);  // foreign districts among the neighbours
             inA &= full;
             // slow_reversible_propose (:117-130): uniform over (node, district) pairs -- slot
             // r < wmax by an exact Lemire map of word 3; the r-th foreign district is the target
-            const uint64_t mw = (uint64_t)slot[256 + lane] * (uint64_t)(uint32_t)p.wmax;
+            const uint64_t mw = (uint64_t)slot[256 + lane] * (uint64_t)(uint32_t)wcap;
             const int r = (int)(mw >> 32);
-            slot_ok = (uint32_t)mw >= p.wthresh && r < __popc(dm);
+            slot_ok = (uint32_t)mw >= wthr && r < __popc(dm);
             uint32_t dd = dm;
             for (int q = 0; q < r && dd; ++q) dd &= dd - 1u;
             tgt = dd ? __builtin_ctz(dd) : 0;
+            nf_after = __popc(dall & ~(1u << tgt));
             tmask = 0;
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) tmask |= (uint32_t)(adv[i] == tgt) << i;
@@ -352,7 +370,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         // packed for the wave-uniform apply
         const uint32_t pk = (uint32_t)v | ((uint32_t)av << 15) | ((uint32_t)tgt << 21) | ((uint32_t)gam << 27);
         const uint32_t pk2 = inA | (nbr << 16);
-        const uint32_t pk3 = tmask | ((uint32_t)(delta + 32) << 16);  // |delta| <= deg <= 16
+        // |delta| <= deg <= 16; nf_after <= 16
+        const uint32_t pk3 = tmask | ((uint32_t)(delta + 32) << 16) | ((uint32_t)nf_after << 24);
         FC_STAMP(t_c);
         FC_PROF(2, t_c - t_b);
 
@@ -467,7 +486,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             const uint32_t pkf = rlu(pk, f), pk2f = rlu(pk2, f), pk3f = rlu(pk3, f);
             const int vf = (int)(pkf & 0x7fffu), Af = (int)((pkf >> 15) & 63u), tf = (int)((pkf >> 21) & 63u);
             const bool gamf = (pkf >> 27) & 1u;
-            const int df = (int)(pk3f >> 16) - 32;
+            const int df = (int)((pk3f >> 16) & 0xffu) - 32;
             const int pvf = rl32(pv, f);
             const uint32_t inAf = pk2f & 0xffffu, nbrf = pk2f >> 16, tmf = pk3f & 0xffffu;
             uint32_t rw[RMAX / 2];
@@ -478,19 +497,65 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((lane >> 1) == k2) ? rw[k2] : sel;
             const int my_e = (int)((sel >> (16 * (lane & 1))) & 0xffffu);
             const bool is_nbr = lane < RMAX && ((nbrf >> lane) & 1u);
-            // foreign-neighbour counts: u sees v leave A (+1 if u in A) and join t (-1 if u in t)
-            const int dlt = (int)((inAf >> lane) & 1u) - (int)((tmf >> lane) & 1u);
-            bool enter = false, leave = false;
-            if (is_nbr && dlt != 0) {
-                const int old = fcnt[my_e];
-                fcnt[my_e] = (uint8_t)(old + dlt);
-                enter = dlt > 0 && old == 0;
-                leave = dlt < 0 && old == 1;
+            bool enter = false, leave = false, grew = false;
+            bool wcap_chg = false;
+            if constexpr (KM == 2) {
+                // foreign-neighbour counts: u sees v leave A (+1 if u in A) and join t (-1 if u in t)
+                const int dlt = (int)((inAf >> lane) & 1u) - (int)((tmf >> lane) & 1u);
+                if (is_nbr && dlt != 0) {
+                    const int old = fcnt[my_e];
+                    fcnt[my_e] = (uint8_t)(old + dlt);
+                    enter = dlt > 0 && old == 0;
+                    leave = dlt < 0 && old == 1;
+                }
+                grew = enter;
+            } else {
+                // foreign districts nf(u) of vf's neighbours, recounted on the new state (v
+                // leaving A can drop A from u's foreign set, joining T add T), and vf's own
+                // from the evaluation; nfh follows every change, and with it the slot bound
+                if (lane == 0) a[vf] = (int8_t)tf;
+                compiler_fence();
+                if (is_nbr) {
+                    const NodeRec<RMAX> ru = G[my_e];
+                    const int au = a[my_e];
+                    const uint32_t nbu = (uint32_t)(ru.meta >> kMetaNbrShift) & 0xffffu;
+                    uint32_t du = 0;
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i)
+                        if ((nbu >> i) & 1u) du |= 1u << a[ring_entry<RMAX>(ru.ring, i)];
+                    const int nfn = __popc(du & ~(1u << au));
+                    const int old = fcnt[my_e];
+                    if (nfn != old) {
+                        fcnt[my_e] = (uint8_t)nfn;
+                        atomicSub(&nfh[old], 1);
+                        atomicAdd(&nfh[nfn], 1);
+                    }
+                    enter = old == 0 && nfn > 0;
+                    leave = old > 0 && nfn == 0;
+                    grew = nfn > old;
+                }
+                if (lane == 0) {
+                    const int old = fcnt[vf], nfn = (int)((pk3f >> 24) & 31u);
+                    if (nfn != old) {
+                        fcnt[vf] = (uint8_t)nfn;
+                        atomicSub(&nfh[old], 1);
+                        atomicAdd(&nfh[nfn], 1);
+                    }
+                }
+                if (p.wdyn) {
+                    compiler_fence();
+                    const uint64_t hm = __ballot(lane >= 1 && lane < kNfh && nfh[lane] > 0);
+                    const int wn = hm ? 63 - __builtin_clzll(hm) : 1;
+                    if (wn != wcap) {  // later draws of the batch map to other slots: end it after f
+                        wcap = wn;
+                        wthr = (0u - (uint32_t)wcap) % (uint32_t)wcap;
+                        wcap_chg = true;
+                    }
+                }
             }
             // non-hit draws to re-check below: nodes that entered the boundary; with PAIR
-            // slots (KM = 0) any node whose foreign-neighbour count grew (its slot may now
-            // fall below it)
-            uint64_t ent = __ballot(KM != 2 ? (is_nbr && dlt > 0) : enter);
+            // slots any node whose foreign-district count grew (its slot may now fall below it)
+            uint64_t ent = __ballot(grew);
             const int dnb = __popcll(__ballot(enter)) - __popcll(__ballot(leave));
             // district-graph tables: the pairs {vf, w} of vf's face-adjacent cells w move from
             // (Af, a[w]) to (tf, a[w]); a count crossing 0 flips an adjacency bit (as does an
@@ -528,9 +593,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 adj_chg = __any(chg);
             }
             if (lane == 0) {
-                a[vf] = (int8_t)tf;
-                fcnt[vf] = (uint8_t)(__popc(nbrf) - __popc(tmf));
-                if constexpr (KM != 2) {
+                if constexpr (KM == 2) {
+                    a[vf] = (int8_t)tf;
+                    fcnt[vf] = (uint8_t)(__popc(nbrf) - __popc(tmf));
+                } else {
                     popk[Af] -= pvf;
                     popk[tf] += pvf;
                 }
@@ -556,6 +622,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             const uint64_t aff = __ballot(hit && lane > f && lane < end);
             if (aff) end = __builtin_ctzll(aff);
             if (adj_chg && f + 1 < end) end = f + 1;
+            if (wcap_chg) {  // every later draw of the batch is re-read under the new bound
+                if (f + 1 < end) end = f + 1;
+                const int t_w = rl32(off_l, f) + 1;
+                if (t_w < trunc_off) trunc_off = t_w;
+            }
             // non-hit draws after f whose node just entered the boundary would now propose
             if (ent) {
                 const int off_f = rl32(off_l, f);
@@ -776,7 +847,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             ga[i] = ((const uint4 *)a)[i];
             gf[i] = ((const uint4 *)fcnt)[i];
         }
-        if (KM != 2 && lane < 32) p.popk[(size_t)c * 32 + lane] = popk[lane];
+        if (KM != 2 && lane < 32) {
+            p.popk[(size_t)c * 32 + lane] = popk[lane];
+            p.nfh[(size_t)c * kNfh + lane] = nfh[lane];
+        }
         if (dgraph) {
             const int kk = p.k * p.k;
             for (int i = lane; i < kk; i += kWave) p.mcnt[(size_t)c * kk + i] = mcnt[i];

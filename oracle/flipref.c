@@ -51,6 +51,17 @@ typedef struct {
     int32_t *eu, *ev;   /* canonical edges (u < v, CSR order) */
 } ctx_t;
 
+/* number of distinct foreign districts among u's neighbours (the PAIR slots of u) */
+static int32_t n_foreign(const ctx_t *c, int32_t u) {
+    const fr_params *p = c->p;
+    uint64_t dm = 0;
+    for (int32_t j = p->row_ptr[u]; j < p->row_ptr[u + 1]; ++j) {
+        const int8_t aw = c->a[p->col_idx[j]];
+        if (aw != c->a[u]) dm |= 1ull << aw;
+    }
+    return (int32_t)__builtin_popcountll(dm);
+}
+
 static int in_boundary(const ctx_t *c, int32_t u) {
     const fr_params *p = c->p;
     for (int32_t j = p->row_ptr[u]; j < p->row_ptr[u + 1]; ++j)
@@ -245,6 +256,8 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
     st->last_flip = -1;
 
     ctx_t c; memset(&c, 0, sizeof c);
+    int32_t *nf = NULL, nfh[65];  /* PAIR: foreign districts per node, and their histogram */
+    memset(nfh, 0, sizeof nfh);
     c.p = p;
     c.a = (int8_t *)malloc((size_t)n);
     c.pops = (int64_t *)calloc((size_t)p->k, sizeof(int64_t));
@@ -298,16 +311,24 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
     yield_state(&c, st, o, 0);                                   /* yield #0 = S0 */
 
     const uint32_t thresh = (uint32_t)((0x100000000ull) % (uint64_t)n);
-    /* PAIR: a global slot count wmax >= every node's number of foreign districts */
-    int32_t wmax = 1;
+    /* PAIR: draw d is a node (word 0) and a slot r < wcap (word 3); it proposes the pair
+     * (v, r-th foreign district of v) iff r < nf(v), the number of v's foreign districts.
+     * Any wcap >= max_u nf(u) makes the proposal uniform over b_nodes' pairs (:151-153).
+     * Canonical stream: wcap = the current state's max_u nf(u) (kept through a histogram of
+     * nf), so compact states waste few slot draws; fc_params.wmax > 0 fixes it instead. */
+    int32_t wcap = 1;
+    const int dyn = p->proposal == FR_PROPOSE_PAIR && p->wmax <= 0;
     if (p->proposal == FR_PROPOSE_PAIR) {
-        int32_t maxdeg = 0;
-        for (int32_t u = 0; u < n; ++u)
-            if (p->row_ptr[u + 1] - p->row_ptr[u] > maxdeg) maxdeg = p->row_ptr[u + 1] - p->row_ptr[u];
-        wmax = p->wmax > 0 ? p->wmax : (maxdeg < p->k - 1 ? maxdeg : p->k - 1);
-        if (wmax < 1) wmax = 1;
+        nf = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+        if (!nf) { rc = -2; goto done; }
+        for (int32_t u = 0; u < n; ++u) { nf[u] = n_foreign(&c, u); nfh[nf[u]] += 1; }
+        if (dyn) {
+            for (int32_t j = 64; j >= 1; --j) if (nfh[j] > 0) { wcap = j; break; }
+        } else {
+            wcap = p->wmax;
+        }
     }
-    const uint32_t wthresh = (uint32_t)((0x100000000ull) % (uint64_t)wmax);
+    uint32_t wthresh = (uint32_t)((0x100000000ull) % (uint64_t)wcap);
     int64_t d = 0;
     while (st->steps < p->n_steps) {
         if ((p->max_draws > 0 && st->draws >= p->max_draws) || (p->tape && d >= p->tape_draws)) {
@@ -329,7 +350,7 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
             /* slow_reversible_propose (:117-130): uniform over (node, foreign district)
              * pairs = uniform node, then slot r < wmax accepted iff r < |D(v)|; D(v) in
              * ascending district order. */
-            const uint64_t mw = (uint64_t)w[3] * (uint64_t)wmax;
+            const uint64_t mw = (uint64_t)w[3] * (uint64_t)wcap;
             if ((uint32_t)mw < wthresh) continue;
             const int32_t r = (int32_t)(mw >> 32);
             uint64_t dm = 0;
@@ -400,6 +421,18 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
             c.nb += after - before;
             st->accepted += 1;
             st->last_flip = v;
+            if (nf) {  /* v's and its neighbours' foreign-district counts, and the slot bound */
+                for (int32_t j = p->row_ptr[v] - 1; j < p->row_ptr[v + 1]; ++j) {
+                    const int32_t u = j < p->row_ptr[v] ? v : p->col_idx[j];
+                    const int32_t f = n_foreign(&c, u);
+                    nfh[nf[u]] -= 1; nfh[f] += 1; nf[u] = f;
+                }
+                if (dyn) {
+                    wcap = 1;
+                    for (int32_t j = 64; j >= 1; --j) if (nfh[j] > 0) { wcap = j; break; }
+                    wthresh = (uint32_t)((0x100000000ull) % (uint64_t)wcap);
+                }
+            }
             st->wait_cur = geom_wait(p, draw, 1, c.nb);
             if (o && o->occupancy) { o->flip_count[v] += 1; o->last_accept[v] = st->steps; }
         }
@@ -422,6 +455,7 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
         }
     }
 done:
+    free(nf);
     free(c.a); free(c.pops); free(c.stamp); free(c.queue); free(c.eu); free(c.ev);
     return rc;
 }

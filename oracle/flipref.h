@@ -79,7 +79,9 @@ typedef struct fr_params {
     int64_t max_draws;         /* stuck cap (<=0: unlimited)                       */
     const double *log1mp;      /* [n+1] log(1-|B|/(N^k-1)); NULL => waits are 0    */
     int32_t proposal;          /* FR_PROPOSE_BI_SIGN (k == 2) or FR_PROPOSE_PAIR   */
-    int32_t wmax;              /* PAIR slot count (<= 0: min(max degree, k - 1))   */
+    int32_t wmax;              /* PAIR slot bound: > 0 a fixed count (>= every node's
+                                  foreign districts); <= 0 the canonical dynamic bound
+                                  = the state's largest foreign-district count      */
     /* accept / constraint variants (grid_chain_sec11.py:39-52,81-110,159-165); zero =
      * Validator([single_flip_contiguous, popbound]) + cut_accept                           */
     int32_t accept;            /* FR_ACCEPT_*                                      */

@@ -327,6 +327,15 @@ def _b_nodes_pairs(partition):  # b_nodes, grid_chain_sec11.py:151-153
     return {(x[0], a[x[1]]) for x in cut}.union({(x[1], a[x[0]]) for x in cut})
 
 
+def _pair_slot_bound(partition):
+    """The canonical PAIR stream's slot bound: the state's largest number of foreign districts
+    of one node (>= 1), i.e. the largest count of b_nodes pairs (:151-153) sharing a node."""
+    cnt: Dict = {}
+    for x, _ in partition["pairs"]:
+        cnt[x] = cnt.get(x, 0) + 1
+    return max(cnt.values(), default=1)
+
+
 def _b_nodes_bi(partition):  # grid_chain_sec11.py:155-156
     return {x[0] for x in partition["cut_edges"]}.union({x[1] for x in partition["cut_edges"]})
 
@@ -381,15 +390,17 @@ class GcFaithfulChain:
         self.log1mp = log1mp
         self.tape = tape
         self.labels = sorted(set(plan.values()))
-        ups = {"population": _population, "cut_edges": _cut_edges, "b_nodes": _b_nodes_bi, "pairs": _b_nodes_pairs}
+        ups = {"population": _population, "cut_edges": _cut_edges, "b_nodes": _b_nodes_bi, "pairs": _b_nodes_pairs,
+               "pair_slots": _pair_slot_bound}
         self.state = _Partition(self.g, assignment=plan, updaters=ups)
         self.d = 0
         self.n = spec.n
         self.thresh = (1 << 32) % self.n
         self.pair = pair
         k = len(self.labels)
-        self.wmax = wmax if wmax > 0 else max(1, min(int(spec.degree().max()), k - 1))
-        self.wthresh = (1 << 32) % self.wmax
+        # slot bound: fixed (wmax > 0) or the canonical dynamic one, the state's largest
+        # foreign-district count (oracle/flipref.c)
+        self.wmax = wmax if wmax > 0 else 0
         self.stats = dict(steps=0, proposals=0, draws=0, accepted=0, inv_contig=0, inv_pop=0,
                           sum_cut=0, sum_nb=0, sum_wait=0)
         self.trace = []
@@ -446,9 +457,10 @@ class GcFaithfulChain:
                 continue
             if self.pair:
                 # slow_reversible_propose (:117-130): uniform over the (node, district) pairs
-                # of b_nodes (:151-153) -- canonical: slot r < wmax, r-th foreign district
-                mw = w[3] * self.wmax
-                if (mw & 0xFFFFFFFF) < self.wthresh:
+                # of b_nodes (:151-153) -- canonical: slot r < wcap, r-th foreign district
+                wcap = self.wmax or s["pair_slots"]
+                mw = w[3] * wcap
+                if (mw & 0xFFFFFFFF) < (1 << 32) % wcap:
                     continue
                 foreign = sorted({d for (x, d) in s["pairs"] if x == node}, key=self.labels.index)
                 r = mw >> 32
