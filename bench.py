@@ -317,6 +317,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--full-diag-steps", type=int, default=3,
                     help="launches of the full-diagnostics side line (0: skip)")
+    ap.add_argument("--acf-yields", type=int, default=10 * 65536,
+                    help="C4 diagnostics leg: yields of the one series window the autocorrelation covers "
+                         "(lags 1 .. 2^16; default 10 x 2^16)")
     ap.add_argument("--tune", default="",
                     help="launch tuning, e.g. nsub=2,hit_stop=24,prio_div=2:5:10 (fc_params.tune_*; "
                          "scheduling only)")
@@ -325,7 +328,7 @@ def main():
     dist, rank, world, local_rank = _dist()
     import torch
     from flipcomplexityempirical_amd import graphs as G
-    from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune
+    from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune, pin_host, unpin_host
     from flipcomplexityempirical_amd import _lib
 
     tune = parse_tune(args.tune) or None
@@ -403,6 +406,11 @@ def main():
         # C4 (BASELINE config 4): the |cut| trace's autocorrelation at lags 1 .. 2^16 and the
         # hitting time of a target |cut| (10 % above the lowest start), on the device, per launch
         c4diag = args.workload == "c4"
+        # C4: one series window over all its launches, long enough for the largest lag (VERDICT
+        # r02 item 5): the leg runs as many launches as --acf-yields needs
+        n_full = args.full_diag_steps
+        if c4diag:
+            n_full = max(n_full, -(-args.acf_yields // args.chain_steps))
         full = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
         if series:
             full |= _lib.FC_DIAG_SERIES
@@ -414,7 +422,8 @@ def main():
             hit = (int(np.ceil(1.1 * cut0)), 10 ** 9)
         cfg_f = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
                           chain_id_offset=int(off), device=local_rank, diag_mask=full, tune=tune,
-                          event_cap=args.chain_steps + 1 if (series or c4diag) else 0, hit_lo=hit[0], hit_hi=hit[1])
+                          event_cap=(n_full * args.chain_steps + 1 if c4diag else args.chain_steps + 1 if series else 0),
+                          hit_lo=hit[0], hit_hi=hit[1])
         lags = [1 << i for i in range(17)]
         rf = FlipRun(fg, inits, cfg_f, bases=bases)
         frame = G.slope_frame(spec, "sec11") if series else None
@@ -425,37 +434,59 @@ def main():
         barrier_sync_f()
         f0 = rf.stats()
         rf.timings()
-        t_series, n_events, n_nan = 0.0, 0, 0
-        t_acf, acf1 = 0.0, []
+        t_series, n_events, n_nan, n_changes = 0.0, 0, 0, 0
+        t_pe, n_pe = 0.0, 0   # the per-event form, measured on the last launch only (outside the rates)
+        cp_buf = None
+        t_acf, acf_out = 0.0, None
         fs_buf = None
         t0f = time.perf_counter()
-        for _ in range(args.full_diag_steps):
+        for it in range(n_full):
             rf.steps(args.chain_steps)
-            if c4diag:
+            if c4diag and it == n_full - 1:  # the whole window: every lag has yields - lag pairs
                 rf.sync()
                 ts = time.perf_counter()
                 _, acf = rf.autocorr(lags)
-                acf1.append(float(np.nanmean(acf[:, 0])))
-                rf.series_reset()
+                pairs = rf.autocorr_pairs(lags)
+                acf_out = {"acf_mean": [float(x) for x in np.nanmean(acf, axis=0)],
+                           "acf_min": [float(x) for x in np.nanmin(acf, axis=0)],
+                           "acf_max": [float(x) for x in np.nanmax(acf, axis=0)],
+                           "pairs_min": [int(x) for x in pairs.min(axis=0)],
+                           "window_yields": int((rf.stats()["steps"] - rf.stats()["series_t0"] + 1).min())}
                 t_acf += time.perf_counter() - ts
             if series:
                 rf.sync()  # the launch is asynchronous: its time must not land in t_series
                 ts = time.perf_counter()
-                if fs_buf is None:  # host buffers reused over the chunks and launches
-                    cap_all = int(rf.stats()["events"].max()) + 1
-                    n_all = 256 * 2 * cap_all  # room for later launches' longer windows
-                    fs_buf = {"slope": np.empty(n_all), "angle": np.empty(n_all),
-                              "n_cut": np.empty(n_all, dtype=np.int32)}
-                for c0 in range(0, C, 256):
-                    fs = rf.frame_series(frame, chains=range(c0, min(C, c0 + 256)),
-                                         out={k: v.reshape(1, -1) for k, v in fs_buf.items()})
-                    n_events += int(fs["len"].sum())
-                    live = np.arange(fs["angle"].shape[1])[None, :] < fs["len"][:, None]  # past len: padding
-                    n_nan += int(np.isnan(fs["angle"][live]).sum())
-                rf.series_reset()
+                # the reference's slope / angle lists (:371-394) as what its plots draw
+                # (:476-484): change points (t, slope, angle) of every chain, on the device, one
+                # copy per array into pinned host buffers reused over the launches
+                if cp_buf is None:
+                    n_cp = 2 * (int(rf.stats()["events"].sum()) + C)
+                    cp_buf = {"t": np.empty(n_cp, dtype=np.int64), "slope": np.empty(n_cp), "angle": np.empty(n_cp)}
+                    for b_ in cp_buf.values():
+                        pin_host(b_)
+                ch = rf.frame_series_changes(frame, out=cp_buf)
+                n_changes += int(ch["offsets"][-1])
+                n_events += int(rf.stats()["events"].sum())
+                n_nan += int(np.isnan(ch["angle"]).sum())
                 t_series += time.perf_counter() - ts
+                if it == n_full - 1:
+                    # beside it, once: the per-event form (every event's slope / angle / frame-cut
+                    # count) copied to the host in chunks of 256 chains
+                    tp = time.perf_counter()
+                    cap_all = int(rf.stats()["events"].max()) + 1
+                    fs_buf = {"slope": np.empty(256 * cap_all), "angle": np.empty(256 * cap_all),
+                              "n_cut": np.empty(256 * cap_all, dtype=np.int32)}
+                    for c0 in range(0, C, 256):
+                        fs = rf.frame_series(frame, chains=range(c0, min(C, c0 + 256)),
+                                             out={k: v.reshape(1, -1) for k, v in fs_buf.items()})
+                        n_pe += int(fs["len"].sum())
+                    t_pe += time.perf_counter() - tp
+                rf.series_reset()
         barrier_sync_f()
-        dtf = D.allreduce_max(time.perf_counter() - t0f, dist, dev)
+        dtf = D.allreduce_max(time.perf_counter() - t0f - t_pe, dist, dev)
+        if cp_buf is not None:
+            for b_ in cp_buf.values():
+                unpin_host(b_)
         kf = D.allreduce_max(float(rf.timings().mean()), dist, dev)
         f1 = rf.stats()
         arrays = {}
@@ -473,26 +504,34 @@ def main():
         yields = int(red["scalars"][:, D.AGG_FIELDS.index("steps")].sum()) + C * world
         t_series = D.allreduce_max(t_series, dist, dev)
         t_acf = D.allreduce_max(t_acf, dist, dev)
-        full_out = {"value": pf / (dtf - t_series - t_acf), "unit": "proposals/s", "launches": args.full_diag_steps,
+        full_out = {"value": pf / (dtf - t_series - t_acf), "unit": "proposals/s", "launches": n_full,
                     "value_with_frame_series_on_host": pf / dtf if series else None,
                     "kernel": rf.kernel_name(), "kernel_ms": kf,
                     "diag": ("waits + accepted-flip log -> |cut| autocorrelation and hitting time on the device "
                              "(BASELINE config 4)" if c4diag else
                              "waits + cut/|B| histograms + per-edge cut_times + per-node flips"
-                             + (" + accepted-flip log -> per-event slope / angle on the device, copied to "
-                                "the host" if series else "")
+                             + (" + accepted-flip log -> slope / angle series (change points) on the device, "
+                                "copied to the host" if series else "")
                              + " (the reference loop body, grid_chain_sec11.py:367-400)"),
-                    "frame_series": {"ms_per_launch": t_series / max(args.full_diag_steps, 1) * 1e3,
-                                     "events": n_events, "events_per_s": n_events / t_series if t_series else None,
-                                     "nan_angles": n_nan,
-                                     "note": "fc_run_frame_series over all chains in chunks of 256, per-event "
-                                             "slope / angle / frame-cut count copied to host arrays"}
+                    "frame_series": {"ms_per_launch": t_series / max(n_full, 1) * 1e3,
+                                     "events": n_events, "change_points": n_changes,
+                                     "events_per_s": n_events / t_series if t_series else None,
+                                     "nan_angles_at_change_points": n_nan,
+                                     "note": "fc_run_frame_series_changes over all chains after every launch: the "
+                                             "(t, slope, angle) change points of the reference's per-yield slope / "
+                                             "angle lists (:371-394), bitwise those lists when held over their "
+                                             "yields (what :476-484 plot), copied into pinned host buffers",
+                                     "per_event_form": {"ms_one_launch": t_pe * 1e3, "entries": n_pe,
+                                                        "note": "fc_run_frame_series (one entry per event, slope / "
+                                                                "angle / frame-cut count) over all chains in chunks "
+                                                                "of 256, last launch only, outside both rates"}}
                     if series else None,
                     "c4_series": {"hit_window": list(hit), "hit_fraction": float((f1["hit_time"] >= 0).mean()),
-                                  "lags": lags, "mean_acf_lag1": acf1,
-                                  "autocorr_ms_per_launch": t_acf / max(args.full_diag_steps, 1) * 1e3,
-                                  "note": "fc_run_autocorr (event log -> per-yield |cut| -> exact lag sums) "
-                                          "after every launch, results copied to the host"}
+                                  "lags": lags, **(acf_out or {}),
+                                  "autocorr_ms": t_acf * 1e3,
+                                  "note": "fc_run_autocorr (event log -> per-yield |cut| -> exact lag sums) over one "
+                                          "series window spanning every launch of the leg (no reset), after the "
+                                          "last launch; acf / pairs per lag over chains (pairs = yields - lag)"}
                     if c4diag else None,
                     "reduced": {"ranks": world, "collectives": "allreduce SUM (scalars, histograms, cut_times, "
                                 "num_flips, part_sum) + allreduce MAX (last_flipped), one row per configuration",

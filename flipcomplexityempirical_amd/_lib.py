@@ -36,7 +36,8 @@ EXPORTED = [
     "fc_run_trace_reset", "fc_run_read_hist", "fc_run_checkpoint", "fc_run_restore",
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_flips_exact", "fc_run_read_wait_expected",
     "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
-    "fc_run_frame_series", "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_destroy",
+    "fc_run_frame_series", "fc_run_frame_series_changes", "fc_host_register", "fc_host_unregister",
+    "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_destroy",
     "fc_device_count", "fc_last_error",
 ]
 
@@ -155,6 +156,10 @@ def load(build_if_missing: bool = True):
     L.fc_run_autocorr.argtypes = [vp, _P(i32), i32, _P(i64), _P(dbl)]
     L.fc_run_frame_series.argtypes = [vp, i32, i32, i32, _P(i32), _P(i32), _P(dbl), dbl, dbl, i64, _P(dbl),
                                       _P(dbl), _P(i32), _P(i64)]
+    L.fc_run_frame_series_changes.argtypes = [vp, i32, i32, i32, _P(i32), _P(i32), _P(dbl), dbl, dbl, i64,
+                                              _P(i64), _P(i64), _P(dbl), _P(dbl)]
+    L.fc_host_register.argtypes = [vp, i64]
+    L.fc_host_unregister.argtypes = [vp]
     L.fc_run_kernel_name.argtypes = [vp, ctypes.c_char_p, i32]
     L.fc_run_n_chains.argtypes = [vp]
     L.fc_run_n_chains.restype = i32

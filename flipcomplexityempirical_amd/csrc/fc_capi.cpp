@@ -1377,6 +1377,119 @@ int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, cons
     return rc;
 }
 
+int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *frame_u,
+                                const int32_t *frame_v, const double *mid_xy, double cx, double cy, int64_t cap,
+                                int64_t *offsets, int64_t *t, double *slope, double *angle) {
+    if (!r || !frame_u || !frame_v || !mid_xy || !offsets)
+        return fail(FC_ERR_ARG, "fc_run_frame_series_changes: null argument");
+    const bool query = !t && !slope && !angle;
+    if (!query && (!t || !slope || !angle)) return fail(FC_ERR_ARG, "fc_run_frame_series_changes: null output");
+    if (!r->d_events) return fail(FC_ERR_ARG, "fc_run_frame_series_changes: FC_DIAG_SERIES not enabled");
+    if (r->p.k != 2) return fail(FC_ERR_UNSUPPORTED, "fc_run_frame_series_changes: k = 2 runs only");
+    if (c0 < 0 || nc < 0 || c0 + nc > r->n_chains) return fail(FC_ERR_ARG, "fc_run_frame_series_changes: chain range");
+    if (n_frame < 0 || n_frame > 256)
+        return fail(FC_ERR_UNSUPPORTED, "fc_run_frame_series_changes: at most 256 frame edges");
+    const int32_t n = r->g.n;
+    std::vector<int32_t> tog_idx(n, -1);
+    std::vector<uint64_t> tog;
+    for (int32_t j = 0; j < n_frame; ++j) {
+        const int32_t ends[2] = {frame_u[j], frame_v[j]};
+        if (ends[0] < 0 || ends[0] >= n || ends[1] < 0 || ends[1] >= n || ends[0] == ends[1])
+            return fail(FC_ERR_ARG, "fc_run_frame_series_changes: frame edge " + std::to_string(j) + " out of range");
+        for (int32_t x : ends) {
+            if (tog_idx[x] < 0) {
+                tog_idx[x] = (int32_t)(tog.size() / 4);
+                tog.insert(tog.end(), 4, 0);
+            }
+            tog[(size_t)tog_idx[x] * 4 + (j >> 6)] |= uint64_t(1) << (j & 63);
+        }
+    }
+    offsets[0] = 0;
+    if (nc == 0) return FC_OK;
+    if (int rc = fc_run_sync(r)) return rc;
+    std::vector<fc::ChainScalars> sc(nc);
+    HIP_TRY(hipMemcpy(sc.data(), r->d_sc + c0, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
+    std::vector<int64_t> ev_len(r->n_chains, 0), t0(r->n_chains, 0);
+    for (int32_t i = 0; i < nc; ++i) {
+        if (sc[i].ev_len > r->ev_cap)
+            return fail(FC_ERR_ARG, "fc_run_frame_series_changes: chain " + std::to_string(c0 + i) +
+                                        " overflowed event_cap; reset the series window more often");
+        ev_len[c0 + i] = sc[i].ev_len;
+        t0[c0 + i] = sc[i].ser_t0;
+    }
+    int32_t *d_fuv = nullptr, *d_tidx = nullptr;
+    int64_t *d_len = nullptr, *d_t0 = nullptr, *d_cnt = nullptr, *d_off = nullptr, *d_t = nullptr;
+    uint64_t *d_tog = nullptr;
+    double *d_mid = nullptr, *d_sa = nullptr;
+    auto cleanup = [&]() {
+        for (void *b : {(void *)d_fuv, (void *)d_tidx, (void *)d_len, (void *)d_t0, (void *)d_cnt, (void *)d_off,
+                        (void *)d_t, (void *)d_tog, (void *)d_mid, (void *)d_sa})
+            if (b) (void)hipFree(b);
+    };
+    auto run = [&]() -> int {
+        int q;
+        if ((q = dalloc(&d_fuv, (size_t)2 * std::max(n_frame, 1)))) return q;
+        if ((q = dalloc(&d_tidx, (size_t)n))) return q;
+        if ((q = dalloc(&d_tog, std::max<size_t>(tog.size(), 4)))) return q;
+        if ((q = dalloc(&d_mid, (size_t)2 * std::max(n_frame, 1)))) return q;
+        if ((q = dalloc(&d_len, (size_t)r->n_chains))) return q;
+        if ((q = dalloc(&d_t0, (size_t)r->n_chains))) return q;
+        if ((q = dalloc(&d_cnt, (size_t)nc))) return q;
+        if ((q = dalloc(&d_off, (size_t)nc))) return q;
+        if (n_frame) {
+            HIP_TRY(hipMemcpy(d_fuv, frame_u, (size_t)n_frame * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(d_fuv + n_frame, frame_v, (size_t)n_frame * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(d_mid, mid_xy, (size_t)n_frame * 16, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(d_tog, tog.data(), tog.size() * 8, hipMemcpyHostToDevice));
+        }
+        HIP_TRY(hipMemcpy(d_tidx, tog_idx.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_len, ev_len.data(), ev_len.size() * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_t0, t0.data(), t0.size() * 8, hipMemcpyHostToDevice));
+        // pass 1: change points per chain -> offsets
+        int e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, d_len, c0, nc, n_frame, d_fuv,
+                                         d_fuv + n_frame, d_mid, cx, cy, d_tidx, d_tog, d_t0, d_cnt, nullptr, nullptr,
+                                         nullptr, nullptr, r->stream);
+        if (e) return fail(FC_ERR_HIP, std::string("frame changes (count): ") + hipGetErrorString((hipError_t)e));
+        std::vector<int64_t> cnt(nc);
+        HIP_TRY(hipMemcpyAsync(cnt.data(), d_cnt, (size_t)nc * 8, hipMemcpyDeviceToHost, r->stream));
+        HIP_TRY(hipStreamSynchronize(r->stream));
+        for (int32_t i = 0; i < nc; ++i) offsets[i + 1] = offsets[i] + cnt[i];
+        const int64_t total = offsets[nc];
+        if (query) return FC_OK;
+        if (cap < total)
+            return fail(FC_ERR_ARG, "fc_run_frame_series_changes: cap " + std::to_string(cap) + " < " +
+                                        std::to_string(total) + " change points (offsets[nc])");
+        // pass 2: (t, slope, angle) at the offsets, then one copy per array
+        if ((q = dalloc(&d_t, (size_t)std::max<int64_t>(total, 1)))) return q;
+        if ((q = dalloc(&d_sa, (size_t)2 * std::max<int64_t>(total, 1)))) return q;
+        HIP_TRY(hipMemcpy(d_off, offsets, (size_t)nc * 8, hipMemcpyHostToDevice));
+        e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, d_len, c0, nc, n_frame, d_fuv,
+                                     d_fuv + n_frame, d_mid, cx, cy, d_tidx, d_tog, d_t0, d_cnt, d_off, d_t, d_sa,
+                                     d_sa + total, r->stream);
+        if (e) return fail(FC_ERR_HIP, std::string("frame changes (write): ") + hipGetErrorString((hipError_t)e));
+        HIP_TRY(hipMemcpyAsync(t, d_t, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
+        HIP_TRY(hipMemcpyAsync(slope, d_sa, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
+        HIP_TRY(hipMemcpyAsync(angle, d_sa + total, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
+        HIP_TRY(hipStreamSynchronize(r->stream));
+        return FC_OK;
+    };
+    const int rc = run();
+    cleanup();
+    return rc;
+}
+
+int fc_host_register(void *ptr, int64_t bytes) {
+    if (!ptr || bytes <= 0) return fail(FC_ERR_ARG, "fc_host_register: null or empty buffer");
+    HIP_TRY(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault));
+    return FC_OK;
+}
+
+int fc_host_unregister(void *ptr) {
+    if (!ptr) return fail(FC_ERR_ARG, "fc_host_unregister: null buffer");
+    HIP_TRY(hipHostUnregister(ptr));
+    return FC_OK;
+}
+
 int fc_run_kernel_name(const fc_run *r, char *buf, int32_t cap) {
     if (!r || !buf || cap <= 0) return fail(FC_ERR_ARG, "fc_run_kernel_name: null argument");
     std::snprintf(buf, (size_t)cap, "%s", r->kname);

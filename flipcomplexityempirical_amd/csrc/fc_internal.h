@@ -218,5 +218,12 @@ int launch_frame_series(const int8_t *a0, int32_t npad, const fc_event *events, 
                         const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
                         const uint64_t *tog_mask, int64_t cap, double *slope, double *angle, int32_t *cnt,
                         void *stream);
+// Change points of the same series (fc_run_frame_series_changes): cp_off == nullptr counts them
+// per chain into cp_cnt[cl]; otherwise writes (t, slope, angle) at cp_off[cl].
+int launch_frame_changes(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
+                         const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
+                         const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
+                         const uint64_t *tog_mask, const int64_t *t0, int64_t *cp_cnt, const int64_t *cp_off,
+                         int64_t *t_out, double *slope, double *angle, void *stream);
 
 }  // namespace fc

@@ -252,6 +252,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             nh += cnt;
         }
         const int ns = nh < 64 ? nh : 64;
+        FC_PROF(17, ns);
+        FC_PROF(18, gen);
         compiler_fence();
         FC_STAMP(t_b);
         FC_PROF(1, t_b - t_a);
@@ -497,6 +499,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((lane >> 1) == k2) ? rw[k2] : sel;
             const int my_e = (int)((sel >> (16 * (lane & 1))) & 0xffffu);
             const bool is_nbr = lane < RMAX && ((nbrf >> lane) & 1u);
+            FC_STAMP(t_g1);
             bool enter = false, leave = false, grew = false;
             bool wcap_chg = false;
             if constexpr (KM == 2) {
@@ -553,6 +556,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                     }
                 }
             }
+            FC_STAMP(t_g2);
+            FC_PROF(9, t_g2 - t_g1);
             // non-hit draws to re-check below: nodes that entered the boundary; with PAIR
             // slots any node whose foreign-district count grew (its slot may now fall below it)
             uint64_t ent = __ballot(grew);
@@ -562,6 +567,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             // outer-face node crossing between districts), which may change the verdict of a
             // later slot: the batch then ends after this flip
             bool adj_chg = false;
+            FC_STAMP(t_g0);
             if (dgraph) {
                 const int Lf = rl32((int)Ln, f);
                 bool chg = false;
@@ -592,6 +598,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 }
                 adj_chg = __any(chg);
             }
+            FC_STAMP(t_g4);
+            FC_PROF(8, t_g4 - t_g0);
             if (lane == 0) {
                 if constexpr (KM == 2) {
                     a[vf] = (int8_t)tf;
@@ -621,6 +629,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             for (int i = 0; i < RMAX; ++i) hit |= v == (int)((rw[i >> 1] >> (16 * (i & 1))) & 0xffffu);
             const uint64_t aff = __ballot(hit && lane > f && lane < end);
             if (aff) end = __builtin_ctzll(aff);
+            FC_PROF(11, aff ? 1 : 0);
+            FC_PROF(15, adj_chg && f + 1 < end ? 1 : 0);
+            FC_PROF(16, wcap_chg && f + 1 < end ? 1 : 0);
             if (adj_chg && f + 1 < end) end = f + 1;
             if (wcap_chg) {  // every later draw of the batch is re-read under the new bound
                 if (f + 1 < end) end = f + 1;
@@ -646,9 +657,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 if (t_na < trunc_off) {
                     trunc_off = t_na;
                     const int e2 = __popcll(__ballot(has && off_l < t_na));
+                    FC_PROF(12, e2 < end ? 1 : 0);
                     if (e2 < end) end = e2;
                 }
             }
+            FC_STAMP(t_g3);
+            FC_PROF(10, t_g3 - t_g2);
             compiler_fence();
             pos = f + 1;
             if (rem == 0) {

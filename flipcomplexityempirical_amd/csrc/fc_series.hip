@@ -143,12 +143,20 @@ __device__ inline void frame_eval(const uint64_t m[kFrameWords], const double *_
     angle = acos(d);
 }
 
+// MODE 0: one (slope, angle, n_cut) entry per event, [cl * cap + i + 1] (entry 0: window start).
+// MODE 1: count the change points of (slope, angle) -- the window start and every event whose
+//         values differ bitwise from the previous entry's -- into cp_cnt[cl].
+// MODE 2: write them at cp_off[cl]: (yield t at which the values start, slope, angle); the
+//         per-yield lists the reference plots (:476-484) are these values held to the next t.
+template <int MODE>
 __global__ __launch_bounds__(kThreads) void frame_series_kernel(
     const int8_t *__restrict__ a0, int32_t npad, const fc_event *__restrict__ events, int64_t ev_cap,
     const int64_t *__restrict__ ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *__restrict__ fu,
     const int32_t *__restrict__ fv, const double *__restrict__ mid, double cx, double cy,
     const int32_t *__restrict__ tog_idx, const uint64_t *__restrict__ tog_mask, int64_t cap,
-    double *__restrict__ slope_out, double *__restrict__ angle_out, int32_t *__restrict__ cnt_out) {
+    double *__restrict__ slope_out, double *__restrict__ angle_out, int32_t *__restrict__ cnt_out,
+    const int64_t *__restrict__ t0, int64_t *__restrict__ cp_cnt, const int64_t *__restrict__ cp_off,
+    int64_t *__restrict__ t_out) {
     const int lane = threadIdx.x & 63;
     const int32_t cl = (int32_t)(blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
     if (cl >= nc) return;  // whole wave
@@ -161,15 +169,38 @@ __global__ __launch_bounds__(kThreads) void frame_series_kernel(
         const bool cut = j < n_frame && a[fu[j]] != a[fv[j]];
         m[w] = __ballot(cut);
     }
-    double *so = slope_out + (size_t)cl * cap, *ao = angle_out + (size_t)cl * cap;
-    int32_t *co = cnt_out + (size_t)cl * cap;
-    if (lane == 0) {
+    double *so = slope_out, *ao = angle_out;
+    int32_t *co = cnt_out;
+    int64_t *to = t_out;
+    if constexpr (MODE == 0) {
+        so += (size_t)cl * cap;
+        ao += (size_t)cl * cap;
+        co += (size_t)cl * cap;
+    } else if constexpr (MODE == 2) {
+        so += cp_off[cl];
+        ao += cp_off[cl];
+        to += cp_off[cl];
+    }
+    // the previous entry's values (bit patterns: NaN == NaN), wave-uniform
+    uint64_t prev_s, prev_a;
+    int64_t pos = 1;  // change points written (the window start is the first)
+    {
         double sl, an;
         int cnt;
         frame_eval(m, mid, cx, cy, sl, an, cnt);
-        so[0] = sl;
-        ao[0] = an;
-        co[0] = cnt;
+        prev_s = (uint64_t)__double_as_longlong(sl);
+        prev_a = (uint64_t)__double_as_longlong(an);
+        if (lane == 0) {
+            if constexpr (MODE == 0) {
+                so[0] = sl;
+                ao[0] = an;
+                co[0] = cnt;
+            } else if constexpr (MODE == 2) {
+                so[0] = sl;
+                ao[0] = an;
+                to[0] = t0[c];
+            }
+        }
     }
     const fc_event *ev = events + (size_t)c * ev_cap;
     const int64_t ne = ev_len[c];
@@ -193,16 +224,42 @@ __global__ __launch_bounds__(kThreads) void frame_series_kernel(
         }
 #pragma unroll
         for (int w = 0; w < kFrameWords; ++w) t[w] ^= m[w];
-        if (i < ne) {
-            double sl, an;
-            int cnt;
-            frame_eval(t, mid, cx, cy, sl, an, cnt);
-            so[i + 1] = sl;
-            ao[i + 1] = an;
-            co[i + 1] = cnt;
+        double sl = 0.0, an = 0.0;
+        int cnt = 0;
+        if (i < ne) frame_eval(t, mid, cx, cy, sl, an, cnt);
+        if constexpr (MODE == 0) {
+            if (i < ne) {
+                so[i + 1] = sl;
+                ao[i + 1] = an;
+                co[i + 1] = cnt;
+            }
+        } else {
+            const uint64_t bs = (uint64_t)__double_as_longlong(sl), ba = (uint64_t)__double_as_longlong(an);
+            uint64_t ps = shfl_up64(bs, 1), pa = shfl_up64(ba, 1);
+            if (lane == 0) {
+                ps = prev_s;
+                pa = prev_a;
+            }
+            const bool chg = i < ne && (bs != ps || ba != pa);
+            const uint64_t cm = __ballot(chg);
+            if constexpr (MODE == 2) {
+                if (chg) {
+                    const int64_t o = pos + __popcll(cm & ((1ull << lane) - 1ull));
+                    so[o] = sl;
+                    ao[o] = an;
+                    to[o] = ev[i].t;
+                }
+            }
+            pos += __popcll(cm);
+            const int last = (int)((ne - b < 64 ? ne - b : 64) - 1);  // the chunk's last event
+            prev_s = (uint64_t)__shfl((long long)bs, last);
+            prev_a = (uint64_t)__shfl((long long)ba, last);
         }
 #pragma unroll
         for (int w = 0; w < kFrameWords; ++w) m[w] = (uint64_t)__shfl((long long)t[w], 63);
+    }
+    if constexpr (MODE == 1) {
+        if (lane == 0) cp_cnt[cl] = pos;
     }
 }
 
@@ -241,8 +298,29 @@ int launch_frame_series(const int8_t *a0, int32_t npad, const fc_event *events, 
     if (n_frame > 64 * kFrameWords) return (int)hipErrorInvalidValue;
     const int wpb = kThreads / 64;
     const dim3 grid((unsigned)((nc + wpb - 1) / wpb));
-    hipLaunchKernelGGL(frame_series_kernel, grid, dim3(kThreads), 0, (hipStream_t)stream, a0, npad, events, ev_cap,
-                       ev_len, c0, nc, n_frame, fu, fv, mid, cx, cy, tog_idx, tog_mask, cap, slope, angle, cnt);
+    hipLaunchKernelGGL(frame_series_kernel<0>, grid, dim3(kThreads), 0, (hipStream_t)stream, a0, npad, events,
+                       ev_cap, ev_len, c0, nc, n_frame, fu, fv, mid, cx, cy, tog_idx, tog_mask, cap, slope, angle, cnt,
+                       (const int64_t *)nullptr, (int64_t *)nullptr, (const int64_t *)nullptr, (int64_t *)nullptr);
+    return (int)hipGetLastError();
+}
+
+int launch_frame_changes(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
+                         const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
+                         const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
+                         const uint64_t *tog_mask, const int64_t *t0, int64_t *cp_cnt, const int64_t *cp_off,
+                         int64_t *t_out, double *slope, double *angle, void *stream) {
+    if (nc <= 0) return (int)hipSuccess;
+    if (n_frame > 64 * kFrameWords) return (int)hipErrorInvalidValue;
+    const int wpb = kThreads / 64;
+    const dim3 grid((unsigned)((nc + wpb - 1) / wpb));
+    if (!cp_off)
+        hipLaunchKernelGGL(frame_series_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, a0, npad, events,
+                           ev_cap, ev_len, c0, nc, n_frame, fu, fv, mid, cx, cy, tog_idx, tog_mask, (int64_t)0,
+                           (double *)nullptr, (double *)nullptr, (int32_t *)nullptr, t0, cp_cnt, cp_off, t_out);
+    else
+        hipLaunchKernelGGL(frame_series_kernel<2>, grid, dim3(kThreads), 0, (hipStream_t)stream, a0, npad, events,
+                           ev_cap, ev_len, c0, nc, n_frame, fu, fv, mid, cx, cy, tog_idx, tog_mask, (int64_t)0, slope,
+                           angle, (int32_t *)nullptr, t0, cp_cnt, cp_off, t_out);
     return (int)hipGetLastError();
 }
 

@@ -37,6 +37,17 @@ def _set_fields(struct, **fields):
         setattr(struct, name, val)
 
 
+def pin_host(arr: np.ndarray) -> np.ndarray:
+    """Page-lock a numpy buffer for the device-to-host copies of the readers
+    (``fc_host_register``); :func:`unpin_host` before it is freed."""
+    check(_lib.load().fc_host_register(ctypes.c_void_p(arr.ctypes.data), int(arr.nbytes)), "fc_host_register")
+    return arr
+
+
+def unpin_host(arr: np.ndarray) -> None:
+    check(_lib.load().fc_host_unregister(ctypes.c_void_p(arr.ctypes.data)), "fc_host_unregister")
+
+
 class FlipGraph:
     """Native graph handle (``fc_graph_create``)."""
 
@@ -389,6 +400,13 @@ class FlipRun:
                                           _p(sums, ctypes.c_int64), _p(acf, ctypes.c_double)), "fc_run_autocorr")
         return sums, acf
 
+    def autocorr_pairs(self, lags: Sequence[int]) -> np.ndarray:
+        """``[n_chains, len(lags)]``: the (t, t + lag) pairs each lag's sum runs over in the
+        current window, max(0, yields - lag) -- a lag at or beyond the window has none."""
+        st = self.stats()
+        n = (st["steps"] - st["series_t0"] + 1).astype(np.int64)
+        return np.maximum(0, n[:, None] - np.asarray(lags, dtype=np.int64)[None, :])
+
     def frame_series(self, frame, chains: Optional[Sequence[int]] = None,
                      out: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
         """Slope / angle of the frame cut edges after every accepted flip of the window, on
@@ -439,6 +457,51 @@ class FlipRun:
         if sel.size == nc and np.array_equal(sel, np.arange(nc)):  # a contiguous range: no copies
             return {"slope": slope, "angle": angle, "n_cut": ncut, "len": ln}
         return {"slope": slope[sel], "angle": angle[sel], "n_cut": ncut[sel], "len": ln[sel]}
+
+    def frame_series_changes(self, frame, c0: int = 0, nc: Optional[int] = None,
+                             out: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
+        """Change points of the slope / angle series of chains ``c0 .. c0 + nc - 1``
+        (``fc_run_frame_series_changes``): ``offsets`` [nc + 1] and flat ``t`` (int64), ``slope``,
+        ``angle`` (float64); chain ``c0 + i`` owns entries ``offsets[i]:offsets[i + 1]``, each
+        value holding from its ``t`` to the next entry's -- what the reference's slope / angle
+        plots draw (``grid_chain_sec11.py:476-484``); :meth:`changes_to_yields` expands one chain
+        to its per-yield lists (``:382,394``).  ``out`` (optional): C-contiguous int64 / float64 /
+        float64 buffers ``t`` / ``slope`` / ``angle`` to fill (e.g. pinned with
+        :func:`pin_host`); used when large enough, the result then holds views of them."""
+        nc = self.n_chains - c0 if nc is None else int(nc)
+        L = _lib.load()
+        eu = np.ascontiguousarray(frame.eu, dtype=np.int32)
+        ev = np.ascontiguousarray(frame.ev, dtype=np.int32)
+        mid = np.ascontiguousarray(frame.mid, dtype=np.float64)
+        off = np.zeros(nc + 1, dtype=np.int64)
+        args = (self.handle, int(c0), nc, int(eu.size), _p(eu, ctypes.c_int32), _p(ev, ctypes.c_int32),
+                _p(mid, ctypes.c_double), float(frame.center[0]), float(frame.center[1]))
+        check(L.fc_run_frame_series_changes(*args, 0, _p(off, ctypes.c_int64), _P(ctypes.c_int64)(),
+                                            _P(ctypes.c_double)(), _P(ctypes.c_double)()), "fc_run_frame_series_changes")
+        total = int(off[-1])
+        bufs = None
+        if out is not None:
+            for key, dt in (("t", np.int64), ("slope", np.float64), ("angle", np.float64)):
+                b = out.get(key)
+                if not isinstance(b, np.ndarray) or b.dtype != dt or not b.flags.c_contiguous or not b.flags.writeable:
+                    raise ValueError(f"frame_series_changes: out[{key!r}] must be a writeable C-contiguous "
+                                     f"{np.dtype(dt)} array")
+            if min(out[key].size for key in ("t", "slope", "angle")) >= total:
+                bufs = {key: out[key].reshape(-1)[:total] for key in ("t", "slope", "angle")}
+        if bufs is None:
+            bufs = {"t": np.empty(total, dtype=np.int64), "slope": np.empty(total), "angle": np.empty(total)}
+        check(L.fc_run_frame_series_changes(*args, total, _p(off, ctypes.c_int64), _p(bufs["t"], ctypes.c_int64),
+                                            _p(bufs["slope"], ctypes.c_double), _p(bufs["angle"], ctypes.c_double)),
+              "fc_run_frame_series_changes")
+        return {"offsets": off, **bufs}
+
+    def changes_to_yields(self, ch: Dict[str, np.ndarray], i: int, chain: int, key: str = "slope") -> np.ndarray:
+        """Per-yield list (the reference's ``slopes`` / ``angles``, :382,394) of ``chain`` from
+        entry ``i`` of a :meth:`frame_series_changes` result."""
+        lo, hi = int(ch["offsets"][i]), int(ch["offsets"][i + 1])
+        T = int(self.stats()["steps"][chain])
+        bounds = np.concatenate([ch["t"][lo:hi], [T + 1]]).astype(np.int64)
+        return np.repeat(ch[key][lo:hi], np.diff(bounds))
 
     def yield_series(self, values: np.ndarray, chain: int = 0) -> np.ndarray:
         """Expand a per-event series (entry 0 = window start, as ``frame_series`` returns it)

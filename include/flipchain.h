@@ -331,6 +331,21 @@ int fc_run_autocorr(fc_run *r, const int32_t *lags, int32_t nlags, int64_t *lag_
 int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *frame_u,
                         const int32_t *frame_v, const double *mid_xy, double cx, double cy, int64_t cap,
                         double *slope, double *angle, int32_t *n_cut, int64_t *len);
+/* Change points of the same slope / angle series: what the reference's slope / angle plots
+ * (grid_chain_sec11.py:476-484, plt.plot(slopes) / plt.plot(angles)) draw, without one entry
+ * per event.  For chain c0 + i, entries offsets[i] .. offsets[i + 1] - 1 hold (t, slope,
+ * angle): the values the per-yield lists (:382,394) take from yield t up to the next entry's t
+ * (the last up to the current yield); the first entry is the window start, and every later one
+ * is an event whose slope or angle differs (bitwise) from the previous entry's.  offsets
+ * [nc + 1] is always filled; with t, slope and angle all NULL the call only sizes the output,
+ * otherwise cap (entries per output array) must be >= offsets[nc] (FC_ERR_ARG).  k = 2 only. */
+int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *frame_u,
+                                const int32_t *frame_v, const double *mid_xy, double cx, double cy, int64_t cap,
+                                int64_t *offsets, int64_t *t, double *slope, double *angle);
+/* Page-lock (pin) a caller's host buffer for faster device-to-host copies of the readers above
+ * (hipHostRegister); unregister before freeing it. */
+int fc_host_register(void *ptr, int64_t bytes);
+int fc_host_unregister(void *ptr);
 /* ---- checkpoint / resume ---------------------------------------------------- */
 /* Everything later fc_run_steps calls depend on -- every chain's assignment, foreign-neighbour
  * counts, draw counter, counters and sums, populations, acceptance thresholds, district-graph

@@ -163,3 +163,29 @@ def test_event_overflow_is_reported(gpu, sec11):
         run.autocorr([1])
     with pytest.raises(OverflowError):
         run.events(0)
+
+
+def test_c4_window_spans_launches_long_lags(gpu, cref):
+    """BASELINE config 4's autocorrelation at long lags: the series window
+    is kept across launches (no reset between them), so lags up to 2^15 have pairs; every lag's
+    exact sum and ACF equal acf_exact on the oracle's per-yield |cut| series of the whole
+    window, and the pair counts are the window length minus the lag."""
+    spec = G.triangular_graph(30, 58)
+    k, steps, launches = 8, 5000, 9
+    plan = G.strip_plan(spec, k)
+    x0 = G.cut_and_boundary(spec, spec.assignment_array(plan, list(range(k))))[0]
+    bases = [0.5, 1.0, 4.0]
+    run, inits = _setup(spec, k, plan, bases, pct=0.1, hit=(1, 0), event_cap=steps * launches + 1)
+    for _ in range(launches):
+        run.steps(steps)
+    lags = [1 << i for i in range(16)]
+    sums, acf = run.autocorr(lags)
+    pairs = run.autocorr_pairs(lags)
+    T = steps * launches + 1
+    assert np.array_equal(pairs, np.maximum(0, T - np.asarray(lags))[None, :].repeat(len(bases), 0))
+    assert (pairs > 0).all()
+    for c, b in enumerate(bases):
+        x = yield_series(_oracle_trace(cref, spec, k, inits[c], b, c, steps * launches, 0.1), x0)
+        assert x.size == T
+        es, ea = acf_exact(x, lags)
+        assert np.array_equal(sums[c], es) and np.array_equal(acf[c], ea)

@@ -138,3 +138,42 @@ def test_frame_series_out_buffers_checked(gpu, sec11):
     small = {k: v[:1] for k, v in good.items()}
     got2 = run.frame_series(frame, out=small)
     assert not np.shares_memory(got2["slope"], good["slope"])
+
+
+@pytest.mark.parametrize("launches", [1, 3])
+def test_frame_series_changes_equal_per_yield_lists(gpu, sec11, launches):
+    """The change-point form of the slope / angle series (fc_run_frame_series_changes): expanded
+    to one value per yield it is bitwise the per-event series held over each event's yields --
+    the reference's slopes / angles lists (:382,394), which its plots draw (:476-484) -- for
+    every chain, over a window spanning several launches, on a chunk of chains not starting at 0;
+    and it is much shorter than one entry per event."""
+    bases = [0.1, 0.8, 1.0, G.SEC11_MU, 10.0, 0.3, 4.0, 2.0]
+    plans = [G.sec11_plan(c % 3, sec11.nodes) for c in range(len(bases))]
+    run, _ = _run(sec11, plans, bases, 0.1)
+    for _ in range(launches):
+        run.steps(1500)
+    frame = G.slope_frame(sec11, "sec11")
+    dense = run.frame_series(frame)
+    ch = run.frame_series_changes(frame, c0=2, nc=5)
+    assert ch["offsets"][0] == 0 and np.all(np.diff(ch["offsets"]) >= 1)
+    n_events = int(dense["len"][2:7].sum())
+    assert ch["offsets"][-1] < n_events
+    for i, c in enumerate(range(2, 7)):
+        for key in ("slope", "angle"):
+            want = run.yield_series(dense[key][c], c)
+            got = run.changes_to_yields(ch, i, c, key)
+            assert got.shape == want.shape
+            assert np.array_equal(got.view(np.int64), want.view(np.int64)), (c, key)
+    n = int(ch["offsets"][-1])
+    pinned = {"t": np.empty(n + 10, dtype=np.int64), "slope": np.empty(n + 10), "angle": np.empty(n + 10)}
+    from flipcomplexityempirical_amd.engine import pin_host, unpin_host
+    for b in pinned.values():
+        pin_host(b)
+    try:
+        ch2 = run.frame_series_changes(frame, c0=2, nc=5, out=pinned)
+        assert np.shares_memory(ch2["t"], pinned["t"])
+        for key in ("t", "slope", "angle"):
+            assert np.array_equal(ch2[key].view(np.int64), ch[key].view(np.int64)), key
+    finally:
+        for b in pinned.values():
+            unpin_host(b)

@@ -1,0 +1,19 @@
+"""Phase cycles of the k > 2 kernel (FC_PHASE_PROF build, FC_PROF_OUT dump of tools/probe_side.py)
+per base group: python tools/prof_side_report.py FILE n_chains n_groups"""
+import sys
+
+import numpy as np
+
+raw = np.fromfile(sys.argv[1], dtype=np.int64)
+C, G = int(sys.argv[2]), int(sys.argv[3]) if len(sys.argv) > 3 else 1
+last = raw.reshape(-1, C, 24)[-1].astype(np.float64)
+for g in range(G):
+    x = last[np.arange(C) % G == g].mean(axis=0)
+    b, fl = max(x[5], 1), max(x[7], 1)
+    print(f"group {g}: total {x[0] / 1e6:.2f} Mcyc  batches {x[5]:.0f}  flips {x[7]:.0f}  commit iters {x[6]:.0f}")
+    print(f"  per batch: draws-gen {x[18] / b:.1f}  slots {x[17] / b:.1f}  cycles: draws {x[1] / b:.0f}  eval {x[2] / b:.0f}"
+          f"  commit {x[3] / b:.0f}  book {x[4] / b:.0f}")
+    print(f"  per flip: dgraph tables {x[8] / fl:.0f}  nf recount {x[9] / fl:.0f}  rest-to-ent {x[10] / fl:.0f}"
+          f"  commit/flip {x[3] / fl:.0f}")
+    print(f"  batch ends: stale view {x[11] / b:.3f}  entering non-hit {x[12] / b:.3f}  adj change {x[15] / b:.3f}"
+          f"  slot-bound change {x[16] / b:.3f}")
