@@ -178,3 +178,31 @@ def test_recom_oracle_keeps_plans_valid(cref, sec11):
     cut, nb, pops = G.cut_and_boundary(sec11, r["final"])
     assert (cut, nb) == (s["cut"], s["nb"]) and lo <= pops.min() and pops.max() <= hi
     assert np.all(np.abs(np.array([pops[0], pops[1]]) - sec11.n / 2) < 0.05 * sec11.n / 2)
+
+
+def test_c_oracle_pair_slot_bound_long_chain(cref):
+    """The canonical PAIR slot bound (the state's largest foreign-district count; oracle/flipref.c)
+    over 10,000 steps of a k = 5 triangular chain at base 1 (every valid proposal accepted, so
+    the bound moves often): the C restatement equals the gerrychain-faithful one draw for draw,
+    and a fixed bound (wmax) wastes more slot draws."""
+    from oracle.flipref import GcFaithfulChain
+    spec = G.triangular_graph(10, 18)
+    k = 5
+    plan = G.strip_plan(spec, k)
+    labels = list(range(k))
+    a0 = spec.assignment_array(plan, labels)
+    l1 = G.log1mp_table(spec.n, k)
+    (lo, hi), (ilo, ihi) = G.population_bounds(int(spec.pop.sum()), k, 0.3)
+    steps = 10000
+    gc = GcFaithfulChain(spec, plan, base=1.0, pop_bounds=(lo, hi), seed=9, chain_id=3, log1mp=l1,
+                         pair=True).run(steps)
+    r = cref.run(spec, a0, base=1.0, pop_lo=ilo, pop_hi=ihi, seed=9, chain_id=3, n_steps=steps, k=k,
+                 labels=labels, log1mp=l1, trace_cap=200000, proposal=1)
+    gtr = np.array(gc.trace, dtype=np.int64)
+    assert len(r["trace"]) == len(gtr)
+    for i, f in enumerate(["draw", "v", "flags", "cut", "nb", "wait"]):
+        assert np.array_equal(r["trace"][f], gtr[:, i]), f
+    assert np.array_equal(gc.assignment_ids(), r["final"])
+    fixed = cref.run(spec, a0, base=1.0, pop_lo=ilo, pop_hi=ihi, seed=9, chain_id=3, n_steps=steps, k=k,
+                     labels=labels, log1mp=l1, proposal=1, wmax=k - 1)
+    assert fixed["stats"]["draws"] > r["stats"]["draws"]  # the fixed bound wastes more slot draws

@@ -285,3 +285,18 @@ def test_enclave_states_district_rule(gpu, cref, flags):
     want = "fc::flip_kernel<8, 2, 0, " if flags else "fc::flip_kernel<8, 2, 3, "
     assert run.kernel_name().startswith(want), run.kernel_name()
     _check(cref, spec, run, k, inits, bases, steps=600, pct=0.95)
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_pair_slot_bound_long_chain_across_launches(gpu, cref, chunks):
+    """The canonical PAIR slot bound (the state's largest foreign-district count,
+    kept per chain as a histogram) over 9,000 steps, in one launch and in three: flips move the
+    bound and end their batch when they do, and every proposal matches the oracle (base 1:
+    every valid proposal accepted)."""
+    spec = G.triangular_graph(20, 38)
+    k = 6
+    a0 = spec.assignment_array(G.strip_plan(spec, k), list(range(k)))
+    inits = np.stack([a0] * 6)
+    bases = np.asarray([1.0, 0.5, 1.0, 3.0, 1.0, 0.25])
+    run = _run_pair(spec, inits, bases, k, steps=9000, pct=0.3, chunks=chunks)
+    _check(cref, spec, run, k, inits, bases, steps=9000, pct=0.3)

@@ -13,7 +13,7 @@ for g in range(G):
     print(f"group {g}: total {x[0] / 1e6:.2f} Mcyc  batches {x[5]:.0f}  flips {x[7]:.0f}  commit iters {x[6]:.0f}")
     print(f"  per batch: draws-gen {x[18] / b:.1f}  slots {x[17] / b:.1f}  cycles: draws {x[1] / b:.0f}  eval {x[2] / b:.0f}"
           f"  commit {x[3] / b:.0f}  book {x[4] / b:.0f}")
-    print(f"  per flip: dgraph tables {x[8] / fl:.0f}  nf recount {x[9] / fl:.0f}  rest-to-ent {x[10] / fl:.0f}"
-          f"  commit/flip {x[3] / fl:.0f}")
+    print(f"  per flip: dgraph tables {x[8] / fl:.0f}  nf update {x[9] / fl:.0f}  rest-to-ent {x[10] / fl:.0f}"
+          f"  commit/flip {x[3] / fl:.0f}  neighbours recounted {x[19] / fl:.2f}")
     print(f"  batch ends: stale view {x[11] / b:.3f}  entering non-hit {x[12] / b:.3f}  adj change {x[15] / b:.3f}"
           f"  slot-bound change {x[16] / b:.3f}")
