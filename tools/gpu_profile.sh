@@ -23,4 +23,12 @@ for w in c3 c4 c5; do
   timeout -k 10 300 python3 bench.py --workload $w --steps 5 --warmup 1 --chain-steps 20000 --no-cpu-baseline --full-diag-steps $FD > "$OUT/side_$w.json" 2> "$OUT/side_$w.err" || { echo "side $w failed"; tail -20 "$OUT/side_$w.err"; exit 1; }
   cat "$OUT/side_$w.json"
 done
+# counters of the k > 2 instances (C4 flip_kernel<8,2,3,false>, C5 flip_kernel<16,4,3,false>)
+for w in c4 c5; do
+  SB="bench.py --workload $w --steps 2 --warmup 1 --chain-steps 20000 --no-cpu-baseline --full-diag-steps 0"
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 300 rocprofv3 --pmc $C -d "$OUT/side_pmc_${w}_$C" -o pmc --output-format csv -- python3 $SB > "$OUT/side_pmc_${w}_$C.log" 2>&1 || { echo "side pmc $w $C failed"; tail -20 "$OUT/side_pmc_${w}_$C.log"; exit 1; }
+  done
+  timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/side_pmc_${w}_lds" -o pmc --output-format csv -- python3 $SB > "$OUT/side_pmc_${w}_lds.log" 2>&1 || { echo "side pmc lds $w failed"; tail -20 "$OUT/side_pmc_${w}_lds.log"; exit 1; }
+done
 echo PROFILE_OK

@@ -73,30 +73,37 @@ json.dump(traffic, open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w"), inde
 check["hbm_bytes_per_launch"] = traffic["hbm_bytes_per_launch"]
 check["hbm_gbs_measured"] = traffic["hbm_bytes_per_launch"] / (statistics.mean(timed) * 1e-3) / 1e9
 
-by = defaultdict(dict)
-for r in flip_rows(os.path.join(src, "pmc_lds", "pmc_counter_collection.csv")):
-    if not "fc::flip2_kernel" in r["Kernel_Name"]:
-        continue
-    d = int(r["Dispatch_Id"])
-    by[d][r["Counter_Name"]] = float(r["Counter_Value"])
-    by[d]["_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
-ids = sorted(by)[1:] or sorted(by)
-avg = {k: statistics.mean(by[i][k] for i in ids) for k in by[ids[0]]}
-t = avg["_ns"] * 1e-9
-clk = avg["GRBM_GUI_ACTIVE"] / 8 / t
-cyc = clk * t
-lds = {"round": tag, "kernel": check["kernel"], "dispatches": len(ids), "kernel_ms": t * 1e3,
-       "counters_per_dispatch": {k: v for k, v in avg.items() if not k.startswith("_")},
-       "effective_clock_ghz": clk / 1e9,
-       "lds_array_busy_frac": avg["SQ_LDS_IDX_ACTIVE"] / (256 * cyc),
-       "lds_bytes_upper_bound_gbs": avg["SQ_LDS_IDX_ACTIVE"] * 256 / t / 1e9,
-       "lds_bank_conflict_frac_of_active": avg["SQ_LDS_BANK_CONFLICT"] / max(avg["SQ_LDS_IDX_ACTIVE"], 1),
-       "valu_insts_per_simd_cycle": avg["SQ_INSTS_VALU"] / (1024 * cyc),
-       "salu_insts_per_cu_cycle": avg["SQ_INSTS_SALU"] / (256 * cyc),
-       "lds_insts_per_wave": avg["SQ_INSTS_LDS"] / max(avg["SQ_WAVES"], 1),
-       "valu_insts_per_wave": avg["SQ_INSTS_VALU"] / max(avg["SQ_WAVES"], 1),
-       "note": "SQ_LDS_IDX_ACTIVE counts LDS-array cycles (incl. bank-conflict cycles) summed over CUs; "
-               "x 256 B/clk/CU bounds the LDS bytes moved from above"}
+def lds_issue(path, kname):
+    """Per-dispatch LDS / issue counters of the kernels named like `kname` (warmup dropped)."""
+    by = defaultdict(dict)
+    names = {}
+    for r in flip_rows(path):
+        if kname not in r["Kernel_Name"]:
+            continue
+        d = int(r["Dispatch_Id"])
+        names[d] = r["Kernel_Name"]
+        by[d][r["Counter_Name"]] = float(r["Counter_Value"])
+        by[d]["_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    ids = sorted(by)[1:] or sorted(by)
+    avg = {k: statistics.mean(by[i][k] for i in ids) for k in by[ids[0]]}
+    t = avg["_ns"] * 1e-9
+    clk = avg["GRBM_GUI_ACTIVE"] / 8 / t
+    cyc = clk * t
+    return {"round": tag, "kernel": names[ids[0]], "dispatches": len(ids), "kernel_ms": t * 1e3,
+           "counters_per_dispatch": {k: v for k, v in avg.items() if not k.startswith("_")},
+           "effective_clock_ghz": clk / 1e9,
+           "lds_array_busy_frac": avg["SQ_LDS_IDX_ACTIVE"] / (256 * cyc),
+           "lds_bytes_upper_bound_gbs": avg["SQ_LDS_IDX_ACTIVE"] * 256 / t / 1e9,
+           "lds_bank_conflict_frac_of_active": avg["SQ_LDS_BANK_CONFLICT"] / max(avg["SQ_LDS_IDX_ACTIVE"], 1),
+           "valu_insts_per_simd_cycle": avg["SQ_INSTS_VALU"] / (1024 * cyc),
+           "salu_insts_per_cu_cycle": avg["SQ_INSTS_SALU"] / (256 * cyc),
+           "lds_insts_per_wave": avg["SQ_INSTS_LDS"] / max(avg["SQ_WAVES"], 1),
+           "valu_insts_per_wave": avg["SQ_INSTS_VALU"] / max(avg["SQ_WAVES"], 1),
+           "note": "SQ_LDS_IDX_ACTIVE counts LDS-array cycles (incl. bank-conflict cycles) summed over CUs; "
+                   "x 256 B/clk/CU bounds the LDS bytes moved from above"}
+
+
+lds = lds_issue(os.path.join(src, "pmc_lds", "pmc_counter_collection.csv"), "fc::flip2_kernel")
 json.dump(lds, open(os.path.join(dst, f"{tag}_lds_issue.json"), "w"), indent=1)
 check["lds_array_busy_frac"] = lds["lds_array_busy_frac"]
 json.dump(check, open(os.path.join(dst, f"{tag}_roofline_check.json"), "w"), indent=1)
@@ -105,4 +112,20 @@ for w in ("c3", "c4", "c5"):
     if os.path.exists(p):
         line = json.loads(open(p).read().strip().splitlines()[-1])
         json.dump(line, open(os.path.join(dst, f"{tag}_side_{w}.json"), "w"), indent=1)
+for w in ("c4", "c5"):  # counters of the k > 2 instances
+    d = os.path.join(src, f"side_pmc_{w}_lds", "pmc_counter_collection.csv")
+    if not os.path.exists(d):
+        continue
+    side = lds_issue(d, "fc::flip_kernel")
+    hb = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        rows = [r for r in flip_rows(os.path.join(src, f"side_pmc_{w}_{c}", "pmc_counter_collection.csv"))
+                if "fc::flip_kernel" in r["Kernel_Name"]]
+        hb[c] = statistics.mean([float(r["Counter_Value"]) for r in rows][1:] or [float(r["Counter_Value"]) for r in rows])
+    side["FETCH_SIZE_KiB_per_launch"] = hb["FETCH_SIZE"]
+    side["WRITE_SIZE_KiB_per_launch"] = hb["WRITE_SIZE"]
+    side["hbm_bytes_per_launch"] = (2 * hb["FETCH_SIZE"] + hb["WRITE_SIZE"]) * 1024
+    side["hbm_gbs_measured"] = side["hbm_bytes_per_launch"] / (side["kernel_ms"] * 1e-3) / 1e9
+    side["workload"] = w
+    json.dump(side, open(os.path.join(dst, f"{tag}_side_pmc_{w}.json"), "w"), indent=1)
 print(json.dumps(check, indent=1))
