@@ -320,6 +320,11 @@ def main():
     ap.add_argument("--acf-yields", type=int, default=10 * 65536,
                     help="C4 diagnostics leg: yields of the one series window the autocorrelation covers "
                          "(lags 1 .. 2^16; default 10 x 2^16)")
+    ap.add_argument("--stream", default="auto", choices=["auto", "band", "node"],
+                    help="k = 2 node stream (fc_params.stream, DESIGN.md §2): auto = node (the band stream "
+                         "measured slower on C2, DESIGN.md §8)")
+    ap.add_argument("--node-stream-steps", type=int, default=3,
+                    help="k = 2 band runs: launches of the node-stream comparison line (0: skip)")
     ap.add_argument("--tune", default="",
                     help="launch tuning, e.g. nsub=2,hit_stop=24,prio_div=2:5:10 (fc_params.tune_*; "
                          "scheduling only)")
@@ -333,6 +338,7 @@ def main():
 
     tune = parse_tune(args.tune) or None
     W = Workload(args.workload)
+    stream = "node" if args.stream == "auto" else args.stream
     spec = W.spec
     fg = FlipGraph(spec)
     from flipcomplexityempirical_amd import distributed as D
@@ -347,7 +353,7 @@ def main():
     bases = np.asarray([W.base_of(int(g)) for g in gids])
     _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), W.k, W.pct)
     cfg = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
-                    chain_id_offset=int(off), device=local_rank, tune=tune)
+                    chain_id_offset=int(off), device=local_rank, tune=tune, stream=stream)
     run = FlipRun(fg, inits, cfg, bases=bases)
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
@@ -391,6 +397,35 @@ def main():
     kernel_ms = D.allreduce_max(kernel_ms, dist, dev)
     props, steps, acc = (float(agg[:, D.AGG_FIELDS.index(k)].sum()) for k in ("proposals", "steps", "accepted"))
 
+    node_out = None
+    if stream == "band" and args.node_stream_steps > 0:
+        # beside it (outside the timed region): the same workload on the node stream, whose draws
+        # range over all n nodes (the round-2 kernel's stream)
+        run.close()
+        rn = FlipRun(fg, inits, RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed,
+                                          pop_lo=lo, pop_hi=hi, chain_id_offset=int(off), device=local_rank,
+                                          tune=tune, stream="node"), bases=bases)
+        rn.steps(args.chain_steps)
+        rn.sync()
+        if dist is not None:
+            dist.barrier()
+        n0 = rn.stats()
+        rn.timings()
+        tn0 = time.perf_counter()
+        for _ in range(args.node_stream_steps):
+            rn.steps(args.chain_steps)
+        rn.sync()
+        if dist is not None:
+            dist.barrier()
+        dtn = D.allreduce_max(time.perf_counter() - tn0, dist, dev)
+        n1 = rn.stats()
+        pn = float(D.allreduce_sum(np.asarray([float((n1["proposals"] - n0["proposals"]).sum())]), dist, dev)[0])
+        dn = float(D.allreduce_sum(np.asarray([float((n1["draws"] - n0["draws"]).sum())]), dist, dev)[0])
+        node_out = {"value": pn / dtn, "unit": "proposals/s", "launches": args.node_stream_steps,
+                    "kernel": rn.kernel_name(), "kernel_ms": D.allreduce_max(float(rn.timings().mean()), dist, dev),
+                    "draws_per_proposal": dn / pn if pn else None}
+        rn.close()
+
     full_out = None
     if args.full_diag_steps > 0:
         # side line, outside the timed region above and on every rank: the same workload with
@@ -421,7 +456,7 @@ def main():
             cut0 = min(G.cut_and_boundary(spec, inits[c])[0] for c in range(0, len(inits), max(1, len(inits) // 64)))
             hit = (int(np.ceil(1.1 * cut0)), 10 ** 9)
         cfg_f = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
-                          chain_id_offset=int(off), device=local_rank, diag_mask=full, tune=tune,
+                          chain_id_offset=int(off), device=local_rank, diag_mask=full, tune=tune, stream=stream,
                           event_cap=(n_full * args.chain_steps + 1 if c4diag else args.chain_steps + 1 if series else 0),
                           hit_lo=hit[0], hit_hi=hit[1])
         lags = [1 << i for i in range(17)]
@@ -429,6 +464,15 @@ def main():
         frame = G.slope_frame(spec, "sec11") if series else None
         rf.steps(args.chain_steps)
         barrier_sync_f = lambda: (rf.sync(), dist.barrier() if dist is not None else None)  # noqa: E731
+        cp_buf = None
+        if series:
+            # setup, once, outside the timed leg: host buffers for the change points, sized from
+            # the warmup launch's count (+50 %), page-locked (a per-launch pin would dominate)
+            n_cp = int(rf.frame_series_changes(frame, query=True)["offsets"][-1])
+            n_cp = n_cp + n_cp // 2 + 4 * C
+            cp_buf = {"t": np.empty(n_cp, dtype=np.int64), "slope": np.empty(n_cp), "angle": np.empty(n_cp)}
+            for b_ in cp_buf.values():
+                pin_host(b_)
         if series or c4diag:
             rf.series_reset()
         barrier_sync_f()
@@ -436,7 +480,6 @@ def main():
         rf.timings()
         t_series, n_events, n_nan, n_changes = 0.0, 0, 0, 0
         t_pe, n_pe = 0.0, 0   # the per-event form, measured on the last launch only (outside the rates)
-        cp_buf = None
         t_acf, acf_out = 0.0, None
         fs_buf = None
         t0f = time.perf_counter()
@@ -459,11 +502,6 @@ def main():
                 # the reference's slope / angle lists (:371-394) as what its plots draw
                 # (:476-484): change points (t, slope, angle) of every chain, on the device, one
                 # copy per array into pinned host buffers reused over the launches
-                if cp_buf is None:
-                    n_cp = 2 * (int(rf.stats()["events"].sum()) + C)
-                    cp_buf = {"t": np.empty(n_cp, dtype=np.int64), "slope": np.empty(n_cp), "angle": np.empty(n_cp)}
-                    for b_ in cp_buf.values():
-                        pin_host(b_)
                 ch = rf.frame_series_changes(frame, out=cp_buf)
                 n_changes += int(ch["offsets"][-1])
                 n_events += int(rf.stats()["events"].sum())
@@ -569,7 +607,7 @@ def main():
         try:
             tj = json.load(open(tfile))
             if (tj.get("chains") == C and tj.get("chain_steps") == args.chain_steps
-                    and tj.get("workload", "c2") == args.workload):
+                    and tj.get("workload", "c2") == args.workload and kname in str(tj.get("kernel"))):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -578,10 +616,10 @@ def main():
         "value": value, "unit": "proposals/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int8",
-        "data": W.data,
+        "data": W.data + (" (band node stream: draws over b_nodes + neighbours)" if stream == "band" else ""),
         "config": {"workload": W.desc, "graph": args.workload, "k": W.k, "chains_per_gpu": C,
                    "chain_steps_per_launch": args.chain_steps,
-                   "parallelism": f"chains sharded over {world} GPU(s)", "tune": tune},
+                   "parallelism": f"chains sharded over {world} GPU(s)", "tune": tune, "stream": stream},
         "steps_per_s": steps / elapsed,
         "per_base_proposals_per_s": {f"{b:.4g}": float(agg[i, 0]) / elapsed for i, b in enumerate(W.bases)},
         "accept_per_proposal": acc / props if props else None,
@@ -607,6 +645,8 @@ def main():
     }
     if full_out is not None:
         out["full_diagnostics"] = full_out
+    if node_out is not None:
+        out["node_stream"] = node_out
     if world == 1 and not args.no_cpu_baseline:
         # one process per CPU this job can use: every host core, unless the affinity set or a
         # cgroup quota grants fewer (then the host's figure is stated as an extrapolation)

@@ -12,7 +12,8 @@ from . import build as _build
 
 _P = ctypes.POINTER
 
-FC_ABI_VERSION = 3  # include/flipchain.h: fc_params layout version
+STREAM_NODE, STREAM_BAND = 0, 1  # include/flipchain.h FC_STREAM_*
+FC_ABI_VERSION = 4  # include/flipchain.h: fc_params layout version
 
 FC_OK = 0
 FC_ERR_ARG = -1
@@ -67,7 +68,9 @@ class Params(ctypes.Structure):
                 ("tune_prio_th", ctypes.c_float * 3), ("tune_search_waves", ctypes.c_int32),
                 ("tune_deal", ctypes.c_int32),
                 # per-chain configuration
-                ("chain_pop_bounds", _P(ctypes.c_int64))]
+                ("chain_pop_bounds", _P(ctypes.c_int64)),
+                # k = 2 node stream: FC_STREAM_NODE / FC_STREAM_BAND
+                ("stream", ctypes.c_int32)]
 
 
 class ChainStats(ctypes.Structure):

@@ -48,6 +48,7 @@ struct fc_run {
     int64_t *d_flip_count = nullptr, *d_occ_acc = nullptr, *d_last_accept = nullptr;  // FC_DIAG_FLIPS_EXACT
     int32_t *d_popk = nullptr;
     int32_t *d_nfh = nullptr;   // k > 2: per chain, nodes per foreign-district count (PAIR slot bound)
+    uint64_t *d_sbits = nullptr;  // k = 2 band stream: per chain, the band S as a bitmap (words u64)
     int32_t *d_mcnt = nullptr, *d_ngk = nullptr;  // k > 2 district-graph rule tables
     bool dgraph = false;
     int32_t wmax = 1;
@@ -67,6 +68,17 @@ struct fc_run {
     double *d_fs_out = nullptr;  // fc_run_frame_series output (slope, angle), grown on demand
     int32_t *d_fs_cnt = nullptr; // ... frame-cut counts
     size_t fs_cap = 0;           // entries per output array held
+    // fc_run_frame_series_changes, kept across calls (one call per launch in the driver loop):
+    // the frame tables (re-uploaded only when the frame changes), per-chain lengths / window
+    // starts / counts / offsets, and the (t, slope, angle) outputs, grown on demand
+    uint64_t fc_frame_hash = 0;
+    int32_t *d_fc_fuv = nullptr, *d_fc_tidx = nullptr;
+    uint64_t *d_fc_tog = nullptr;
+    double *d_fc_mid = nullptr;
+    int64_t *d_fc_len = nullptr, *d_fc_t0 = nullptr, *d_fc_cnt = nullptr, *d_fc_off = nullptr;
+    int64_t *d_fc_t = nullptr;
+    double *d_fc_sa = nullptr;
+    size_t fc_cap = 0;           // change points the outputs hold
     char kname[96] = {0};        // last launched flip-kernel instance
     uint64_t param_hash = 0;     // FNV-1a of every trajectory-determining parameter (checkpoint check)
     bool variant = false;        // accept / constraint variants (FULL k = 2 instance)
@@ -108,8 +120,9 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_nfh, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh,
-                    r->d_fs_out, r->d_fs_cnt};
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_nfh, r->d_sbits, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh,
+                    r->d_fs_out, r->d_fs_cnt, r->d_fc_fuv, r->d_fc_tidx, r->d_fc_tog, r->d_fc_mid, r->d_fc_len,
+                    r->d_fc_t0, r->d_fc_cnt, r->d_fc_off, r->d_fc_t, r->d_fc_sa};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -270,6 +283,10 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     if (p->proposal != FC_PROPOSE_BI_SIGN && p->proposal != FC_PROPOSE_PAIR && p->proposal != FC_PROPOSE_RECOM)
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: unsupported proposal");
     const bool recom = p->proposal == FC_PROPOSE_RECOM;
+    if (p->stream != FC_STREAM_NODE && p->stream != FC_STREAM_BAND)
+        return fail(FC_ERR_ARG, "fc_run_create: stream must be FC_STREAM_NODE or FC_STREAM_BAND");
+    if (p->stream == FC_STREAM_BAND && (p->k != 2 || recom || gr->h.n > 4096))
+        return fail(FC_ERR_UNSUPPORTED, "fc_run_create: the band stream is for k = 2 flip runs on n <= 4096 nodes");
     if (recom) {
         if (p->accept != FC_ACCEPT_CUT || p->con_valid != 0 || p->con_accept != 0 || p->n_frozen > 0)
             return fail(FC_ERR_UNSUPPORTED, "fc_run_create: recom runs with the population Validator and cut_accept");
@@ -344,7 +361,8 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     else if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, 3 BFS bitmaps, slots, commit marks (2 npad + 16),
                       // wait / tally queue (24 B per entry), launch start time, pace, first queued yield (24)
                       // (sec11: 10,016 B, so 16 chains still fill a CU's 160 KB)
-        r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16 + fc::kWaitQ * 24 + 24;
+        r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16 + fc::kWaitQ * 24 + 24 +
+                             (p->stream == FC_STREAM_BAND ? 8 * r->words : 0);  // the band bitmap (sec11: 200 B)
     // k > 2: with every node's ring exact (all bounded faces triangles / quadrilaterals, so the
     // rings list every face-adjacent cell) contiguity is decided by the district-graph rule
     // (fc_kernels.hip district_rule) instead of the device search, whose scratch is then not
@@ -432,6 +450,8 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     std::vector<fc::ChainScalars> sc(n_chains);
     std::vector<int32_t> popk((size_t)n_chains * fc::kMaxKGeneral, 0);
     std::vector<int32_t> nfh(k > 2 && !recom ? (size_t)n_chains * fc::kNfh : 0, 0);
+    const bool band = p->stream == FC_STREAM_BAND;
+    std::vector<uint64_t> sbits(band ? (size_t)n_chains * r->words : 0, 0);
     std::vector<int32_t> mcnt(r->dgraph ? (size_t)n_chains * k * k : 0, 0), ngk(r->dgraph ? (size_t)n_chains * 32 : 0, 0);
     std::vector<uint64_t> thresh((size_t)n_chains * (2 * R + 1));
     std::vector<int32_t> q;
@@ -479,6 +499,14 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
             }
             fcnt[(size_t)c * r->npad + u] = (uint8_t)f;
             nb += f > 0;
+        }
+        if (band) {  // the band S of the initial state: b_nodes and their neighbours
+            uint64_t *sb = &sbits[(size_t)c * r->words];
+            for (int32_t u = 0; u < n; ++u) {
+                if (!fcnt[(size_t)c * r->npad + u]) continue;
+                sb[u >> 6] |= 1ull << (u & 63);
+                for (int32_t j = g.row_ptr[u]; j < g.row_ptr[u + 1]; ++j) sb[g.col_idx[j] >> 6] |= 1ull << (g.col_idx[j] & 63);
+            }
         }
         fc::ChainScalars &s = sc[c];
         std::memset(&s, 0, sizeof s);
@@ -558,7 +586,8 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         h = fnv1a(h, r->labels.data(), r->labels.size() * 4);
         h = fnv1a(h, r->log1mp.data(), r->log1mp.size() * 8);
         const int64_t scal[] = {k, p->proposal, p->accept, (int64_t)con_valid, (int64_t)p->con_accept, p->flags,
-                                r->wmax, p->hit_lo, p->hit_hi, p->recom_node_repeats, p->recom_max_attempts};
+                                r->wmax, p->hit_lo, p->hit_hi, p->recom_node_repeats, p->recom_max_attempts,
+                                p->stream};
         h = fnv1a(h, scal, sizeof scal);
         const double dscal[] = {p->beta, p->recom_pop_target, p->recom_epsilon, bases ? bases[0] : p->base};
         h = fnv1a(h, dscal, sizeof dscal);
@@ -589,6 +618,10 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     HIP_TRY(hipMemcpy(r->d_fcnt, fcnt.data(), fcnt.size(), hipMemcpyHostToDevice));
     if ((rc = dalloc(&r->d_popk, popk.size()))) return rc;
     HIP_TRY(hipMemcpy(r->d_popk, popk.data(), popk.size() * 4, hipMemcpyHostToDevice));
+    if (band) {
+        if ((rc = dalloc(&r->d_sbits, sbits.size()))) return rc;
+        HIP_TRY(hipMemcpy(r->d_sbits, sbits.data(), sbits.size() * 8, hipMemcpyHostToDevice));
+    }
     if (!nfh.empty()) {
         if ((rc = dalloc(&r->d_nfh, nfh.size()))) return rc;
         HIP_TRY(hipMemcpy(r->d_nfh, nfh.data(), nfh.size() * 4, hipMemcpyHostToDevice));
@@ -672,6 +705,8 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
 
 int fc_run_set_tape(fc_run *r, const uint32_t *tape, int64_t n_draws) {
     if (!r) return fail(FC_ERR_ARG, "fc_run_set_tape: null run");
+    if (r->d_sbits && tape && n_draws > 0)  // a tape's word 0 is a node of all n (the node-tape map)
+        return fail(FC_ERR_ARG, "fc_run_set_tape: replay tapes need the node stream (FC_STREAM_NODE)");
     HIP_TRY(hipSetDevice(r->p.device));
     if (r->d_tape) { HIP_TRY(hipFree(r->d_tape)); r->d_tape = nullptr; }
     r->tape_draws = 0;
@@ -723,6 +758,10 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.wmax = r->wmax > 0 ? r->wmax : 1;
     k.wdyn = r->p.k > 2 && r->wmax <= 0 ? 1 : 0;
     k.nfh = r->d_nfh;
+    k.band = r->d_sbits ? 1 : 0;
+    k.sbits = r->d_sbits;
+    k.band_step0 = 1;
+    while (k.band_step0 * 2 < r->words) k.band_step0 *= 2;
     k.chain_lds_bytes = r->chain_lds_bytes;
     k.words = r->words;
     k.lab_words = fc::bfs_lab_words(r->g.n);
@@ -953,6 +992,7 @@ static std::vector<std::pair<void *, size_t>> ckpt_sections(fc_run *r) {
         v.emplace_back(r->d_fcnt, C * r->npad);
         v.emplace_back(r->d_popk, C * fc::kMaxKGeneral * 4);
         if (r->d_nfh) v.emplace_back(r->d_nfh, C * fc::kNfh * 4);
+        if (r->d_sbits) v.emplace_back(r->d_sbits, C * (size_t)r->words * 8);
         v.emplace_back(r->d_thresh, C * (2 * R + 1) * 8);
         if (r->dgraph) {
             v.emplace_back(r->d_mcnt, C * k * k * 4);
@@ -1390,92 +1430,107 @@ int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_fra
     if (n_frame < 0 || n_frame > 256)
         return fail(FC_ERR_UNSUPPORTED, "fc_run_frame_series_changes: at most 256 frame edges");
     const int32_t n = r->g.n;
-    std::vector<int32_t> tog_idx(n, -1);
-    std::vector<uint64_t> tog;
-    for (int32_t j = 0; j < n_frame; ++j) {
-        const int32_t ends[2] = {frame_u[j], frame_v[j]};
-        if (ends[0] < 0 || ends[0] >= n || ends[1] < 0 || ends[1] >= n || ends[0] == ends[1])
+    for (int32_t j = 0; j < n_frame; ++j)
+        if (frame_u[j] < 0 || frame_u[j] >= n || frame_v[j] < 0 || frame_v[j] >= n || frame_u[j] == frame_v[j])
             return fail(FC_ERR_ARG, "fc_run_frame_series_changes: frame edge " + std::to_string(j) + " out of range");
-        for (int32_t x : ends) {
-            if (tog_idx[x] < 0) {
-                tog_idx[x] = (int32_t)(tog.size() / 4);
-                tog.insert(tog.end(), 4, 0);
-            }
-            tog[(size_t)tog_idx[x] * 4 + (j >> 6)] |= uint64_t(1) << (j & 63);
-        }
-    }
     offsets[0] = 0;
     if (nc == 0) return FC_OK;
     if (int rc = fc_run_sync(r)) return rc;
+    int q;
+    // the frame tables: uploaded when the frame differs from the last call's
+    uint64_t h = fnv1a(0xcbf29ce484222325ull, &n_frame, sizeof n_frame);
+    h = fnv1a(h, frame_u, (size_t)n_frame * 4);
+    h = fnv1a(h, frame_v, (size_t)n_frame * 4);
+    h = fnv1a(h, mid_xy, (size_t)n_frame * 16);
+    if (!r->d_fc_fuv || h != r->fc_frame_hash) {
+        std::vector<int32_t> tog_idx(n, -1);
+        std::vector<uint64_t> tog;
+        for (int32_t j = 0; j < n_frame; ++j) {
+            const int32_t ends[2] = {frame_u[j], frame_v[j]};
+            for (int32_t x : ends) {
+                if (tog_idx[x] < 0) {
+                    tog_idx[x] = (int32_t)(tog.size() / 4);
+                    tog.insert(tog.end(), 4, 0);
+                }
+                tog[(size_t)tog_idx[x] * 4 + (j >> 6)] |= uint64_t(1) << (j & 63);
+            }
+        }
+        for (void *b : {(void *)r->d_fc_fuv, (void *)r->d_fc_tidx, (void *)r->d_fc_tog, (void *)r->d_fc_mid})
+            if (b) (void)hipFree(b);
+        r->d_fc_fuv = r->d_fc_tidx = nullptr;
+        r->d_fc_tog = nullptr;
+        r->d_fc_mid = nullptr;
+        if ((q = dalloc(&r->d_fc_fuv, (size_t)2 * 256))) return q;
+        if ((q = dalloc(&r->d_fc_tidx, (size_t)n))) return q;
+        if ((q = dalloc(&r->d_fc_tog, (size_t)4 * 512))) return q;
+        if ((q = dalloc(&r->d_fc_mid, (size_t)2 * 256))) return q;
+        if (n_frame) {
+            HIP_TRY(hipMemcpy(r->d_fc_fuv, frame_u, (size_t)n_frame * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(r->d_fc_fuv + n_frame, frame_v, (size_t)n_frame * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(r->d_fc_mid, mid_xy, (size_t)n_frame * 16, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(r->d_fc_tog, tog.data(), tog.size() * 8, hipMemcpyHostToDevice));
+        }
+        HIP_TRY(hipMemcpy(r->d_fc_tidx, tog_idx.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        r->fc_frame_hash = h;
+    }
+    if (!r->d_fc_len) {
+        const size_t C = (size_t)r->n_chains;
+        if ((q = dalloc(&r->d_fc_len, C))) return q;
+        if ((q = dalloc(&r->d_fc_t0, C))) return q;
+        if ((q = dalloc(&r->d_fc_cnt, C))) return q;
+        if ((q = dalloc(&r->d_fc_off, C))) return q;
+    }
     std::vector<fc::ChainScalars> sc(nc);
     HIP_TRY(hipMemcpy(sc.data(), r->d_sc + c0, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
-    std::vector<int64_t> ev_len(r->n_chains, 0), t0(r->n_chains, 0);
+    std::vector<int64_t> ev_len(nc), t0(nc);
     for (int32_t i = 0; i < nc; ++i) {
         if (sc[i].ev_len > r->ev_cap)
             return fail(FC_ERR_ARG, "fc_run_frame_series_changes: chain " + std::to_string(c0 + i) +
                                         " overflowed event_cap; reset the series window more often");
-        ev_len[c0 + i] = sc[i].ev_len;
-        t0[c0 + i] = sc[i].ser_t0;
+        ev_len[i] = sc[i].ev_len;
+        t0[i] = sc[i].ser_t0;
     }
-    int32_t *d_fuv = nullptr, *d_tidx = nullptr;
-    int64_t *d_len = nullptr, *d_t0 = nullptr, *d_cnt = nullptr, *d_off = nullptr, *d_t = nullptr;
-    uint64_t *d_tog = nullptr;
-    double *d_mid = nullptr, *d_sa = nullptr;
-    auto cleanup = [&]() {
-        for (void *b : {(void *)d_fuv, (void *)d_tidx, (void *)d_len, (void *)d_t0, (void *)d_cnt, (void *)d_off,
-                        (void *)d_t, (void *)d_tog, (void *)d_mid, (void *)d_sa})
-            if (b) (void)hipFree(b);
-    };
-    auto run = [&]() -> int {
-        int q;
-        if ((q = dalloc(&d_fuv, (size_t)2 * std::max(n_frame, 1)))) return q;
-        if ((q = dalloc(&d_tidx, (size_t)n))) return q;
-        if ((q = dalloc(&d_tog, std::max<size_t>(tog.size(), 4)))) return q;
-        if ((q = dalloc(&d_mid, (size_t)2 * std::max(n_frame, 1)))) return q;
-        if ((q = dalloc(&d_len, (size_t)r->n_chains))) return q;
-        if ((q = dalloc(&d_t0, (size_t)r->n_chains))) return q;
-        if ((q = dalloc(&d_cnt, (size_t)nc))) return q;
-        if ((q = dalloc(&d_off, (size_t)nc))) return q;
-        if (n_frame) {
-            HIP_TRY(hipMemcpy(d_fuv, frame_u, (size_t)n_frame * 4, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(d_fuv + n_frame, frame_v, (size_t)n_frame * 4, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(d_mid, mid_xy, (size_t)n_frame * 16, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(d_tog, tog.data(), tog.size() * 8, hipMemcpyHostToDevice));
-        }
-        HIP_TRY(hipMemcpy(d_tidx, tog_idx.data(), (size_t)n * 4, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(d_len, ev_len.data(), ev_len.size() * 8, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(d_t0, t0.data(), t0.size() * 8, hipMemcpyHostToDevice));
-        // pass 1: change points per chain -> offsets
-        int e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, d_len, c0, nc, n_frame, d_fuv,
-                                         d_fuv + n_frame, d_mid, cx, cy, d_tidx, d_tog, d_t0, d_cnt, nullptr, nullptr,
-                                         nullptr, nullptr, r->stream);
-        if (e) return fail(FC_ERR_HIP, std::string("frame changes (count): ") + hipGetErrorString((hipError_t)e));
-        std::vector<int64_t> cnt(nc);
-        HIP_TRY(hipMemcpyAsync(cnt.data(), d_cnt, (size_t)nc * 8, hipMemcpyDeviceToHost, r->stream));
-        HIP_TRY(hipStreamSynchronize(r->stream));
-        for (int32_t i = 0; i < nc; ++i) offsets[i + 1] = offsets[i] + cnt[i];
-        const int64_t total = offsets[nc];
-        if (query) return FC_OK;
-        if (cap < total)
-            return fail(FC_ERR_ARG, "fc_run_frame_series_changes: cap " + std::to_string(cap) + " < " +
-                                        std::to_string(total) + " change points (offsets[nc])");
-        // pass 2: (t, slope, angle) at the offsets, then one copy per array
-        if ((q = dalloc(&d_t, (size_t)std::max<int64_t>(total, 1)))) return q;
-        if ((q = dalloc(&d_sa, (size_t)2 * std::max<int64_t>(total, 1)))) return q;
-        HIP_TRY(hipMemcpy(d_off, offsets, (size_t)nc * 8, hipMemcpyHostToDevice));
-        e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, d_len, c0, nc, n_frame, d_fuv,
-                                     d_fuv + n_frame, d_mid, cx, cy, d_tidx, d_tog, d_t0, d_cnt, d_off, d_t, d_sa,
-                                     d_sa + total, r->stream);
-        if (e) return fail(FC_ERR_HIP, std::string("frame changes (write): ") + hipGetErrorString((hipError_t)e));
-        HIP_TRY(hipMemcpyAsync(t, d_t, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
-        HIP_TRY(hipMemcpyAsync(slope, d_sa, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
-        HIP_TRY(hipMemcpyAsync(angle, d_sa + total, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
-        HIP_TRY(hipStreamSynchronize(r->stream));
-        return FC_OK;
-    };
-    const int rc = run();
-    cleanup();
-    return rc;
+    // the kernels index the per-chain arrays by global chain id
+    HIP_TRY(hipMemcpyAsync(r->d_fc_len + c0, ev_len.data(), (size_t)nc * 8, hipMemcpyHostToDevice, r->stream));
+    HIP_TRY(hipMemcpyAsync(r->d_fc_t0 + c0, t0.data(), (size_t)nc * 8, hipMemcpyHostToDevice, r->stream));
+    int32_t *const d_fuv = r->d_fc_fuv;
+    // pass 1: change points per chain -> offsets
+    int e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, r->d_fc_len, c0, nc, n_frame, d_fuv,
+                                     d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->d_fc_t0,
+                                     r->d_fc_cnt, nullptr, nullptr, nullptr, nullptr, r->stream);
+    if (e) return fail(FC_ERR_HIP, std::string("frame changes (count): ") + hipGetErrorString((hipError_t)e));
+    std::vector<int64_t> cnt(nc);
+    HIP_TRY(hipMemcpyAsync(cnt.data(), r->d_fc_cnt, (size_t)nc * 8, hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    for (int32_t i = 0; i < nc; ++i) offsets[i + 1] = offsets[i] + cnt[i];
+    const int64_t total = offsets[nc];
+    if (query) return FC_OK;
+    if (cap < total)  // offsets are filled: the caller can size its buffers and call again
+        return fail(FC_ERR_ARG, "fc_run_frame_series_changes: cap " + std::to_string(cap) + " < " +
+                                    std::to_string(total) + " change points (offsets[nc])");
+    if ((size_t)total > r->fc_cap) {
+        if (r->d_fc_t) (void)hipFree(r->d_fc_t);
+        if (r->d_fc_sa) (void)hipFree(r->d_fc_sa);
+        r->d_fc_t = nullptr;
+        r->d_fc_sa = nullptr;
+        r->fc_cap = 0;
+        const size_t want = (size_t)total + (size_t)total / 4 + 1024;  // headroom: one allocation per run
+        if ((q = dalloc(&r->d_fc_t, want))) return q;
+        if ((q = dalloc(&r->d_fc_sa, 2 * want))) return q;
+        r->fc_cap = want;
+    }
+    // pass 2: (t, slope, angle) at the offsets, then one copy per array
+    HIP_TRY(hipMemcpyAsync(r->d_fc_off, offsets, (size_t)nc * 8, hipMemcpyHostToDevice, r->stream));
+    double *const d_sl = r->d_fc_sa, *const d_an = r->d_fc_sa + r->fc_cap;
+    e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, r->d_fc_len, c0, nc, n_frame, d_fuv,
+                                 d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->d_fc_t0, r->d_fc_cnt,
+                                 r->d_fc_off, r->d_fc_t, d_sl, d_an, r->stream);
+    if (e) return fail(FC_ERR_HIP, std::string("frame changes (write): ") + hipGetErrorString((hipError_t)e));
+    HIP_TRY(hipMemcpyAsync(t, r->d_fc_t, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipMemcpyAsync(slope, d_sl, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipMemcpyAsync(angle, d_an, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    return FC_OK;
 }
 
 int fc_host_register(void *ptr, int64_t bytes) {

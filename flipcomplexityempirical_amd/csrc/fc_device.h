@@ -60,6 +60,22 @@ __device__ __forceinline__ int wave_scan_incl(int x) {
     return x + (lane >= 16 ? r0 : 0) + (lane >= 32 ? r1 : 0) + (lane >= 48 ? r2 : 0);
 }
 
+// position of the r-th (0-based) set bit of x, r < popcount(x): five popcount halvings
+__device__ __forceinline__ int select_bit64(uint64_t x, int r) {
+    uint32_t y = (uint32_t)x;
+    int pos = 0, c = __popc(y);
+    if (r >= c) { r -= c; y = (uint32_t)(x >> 32); pos = 32; }
+    c = __popc(y & 0xffffu);
+    if (r >= c) { r -= c; y >>= 16; pos += 16; }
+    c = __popc(y & 0xffu);
+    if (r >= c) { r -= c; y >>= 8; pos += 8; }
+    c = __popc(y & 0xfu);
+    if (r >= c) { r -= c; y >>= 4; pos += 4; }
+    c = __popc(y & 0x3u);
+    if (r >= c) { r -= c; y >>= 2; pos += 2; }
+    return pos + (r >= (int)(y & 1u) ? 1 : 0);
+}
+
 __device__ __forceinline__ int kth_set_bit(uint64_t x, int k) {  // k >= 1
     for (int i = 1; i < k; ++i) x &= x - 1;
     return __builtin_ctzll(x);

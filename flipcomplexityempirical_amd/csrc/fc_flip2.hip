@@ -40,7 +40,12 @@ using namespace dev;
 // rule decides every proposal and the instance carries no search code (its registers are the
 // hot loop's).  XTRA (FULL only): replay tapes, per-proposal traces, accept / constraint
 // variants and frozen nodes; the diagnostics instance without them keeps its registers too.
-template <int RMAX, int NSUB, bool FULL, bool SEARCH, bool XTRA>
+//
+// BAND (FC_STREAM_BAND): a draw picks the i-th member of the chain's band S (b_nodes and their
+// neighbours, an LDS bitmap) instead of one of all n nodes.  S only changes when an accepted flip
+// puts a node outside S into b_nodes; the batch then ends after that flip and S is rebuilt, so
+// within a batch the draw -> node map is fixed, as the speculative evaluation needs.
+template <int RMAX, int NSUB, bool FULL, bool SEARCH, bool XTRA, bool BAND>
 __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams p) {
     static_assert(FULL || !XTRA, "XTRA is a FULL instance");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -66,6 +71,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     uint8_t *smark = (uint8_t *)(slot + 5 * 64);   // [npad] lowest slot of a segment flip at the node
     uint8_t *nmark = smark + npad;                 // [npad] ... having the node as a neighbour
     uint8_t *const dum = nmark + npad + (lane & 15);  // [16] sink for masked-off stores
+    // a store only some lanes make: FC_MASKED_STORES masks the others off (exec mask), else they
+    // write the sink (no branch, but 64 lanes on 16 bytes)
+#ifdef FC_MASKED_STORES
+#define FC_ST(cond, ref, val) \
+    do {                      \
+        if (cond) (ref) = (val); \
+    } while (0)
+#else
+#define FC_ST(cond, ref, val) (*((cond) ? (uint8_t *)&(ref) : dum) = (uint8_t)(val))
+#endif
     // accepted states whose geometric wait is still to be drawn (kWaitQ of them:
     // creating draw, |B| after the flip, yields so far); see wait_flush below
     uint64_t *q_d = (uint64_t *)(nmark + npad + 16);
@@ -76,6 +91,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     // [3]: launch start time, previous launch's pace (read back, not held), yield of the first
     // queued state
     uint64_t *misc = (uint64_t *)(q_c + kWaitQ);
+    uint64_t *const sb = misc + 3;  // BAND: [words] the band S (bit u: node u in S)
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
     // ---- load the chain into LDS -------------------------------------------------------
@@ -88,6 +104,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         }
         if (lane < 2 * RMAX + 1) T[lane] = p.thresh[(size_t)c * (2 * RMAX + 1) + lane];
         for (int i = lane; i < npad / 4 + 2; i += kWave) ((uint64_t *)smark)[i] = ~0ull;  // marks + sink
+        if (BAND && lane < p.words) sb[lane] = p.sbits[(size_t)c * p.words + lane];
     }
     ChainScalars *scp = p.sc + c;
     uint64_t draw = scp->draw;
@@ -121,6 +138,39 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     if (lane < kProfSlots) prof_acc[lane] = 0;
 #endif
     wave_sync();
+    // BAND: |S| and the Lemire threshold 2^32 mod |S| (scalars, changed only by band_rebuild)
+    uint32_t nS = 1u, thrS = 0u;
+    auto band_count = [&]() {
+        const int cw = lane < p.words ? (int)__popcll(sb[lane]) : 0;
+        nS = (uint32_t)rl32(wave_scan_incl(cw), kWave - 1);
+        thrS = (0u - nS) % nS;
+    };
+    // S := b_nodes of the current state and their neighbours (the oracle's band_build)
+    auto band_rebuild = [&]() {
+        compiler_fence();
+        if (lane < p.words) sb[lane] = 0ull;
+        compiler_fence();
+        for (int j = 0; j < p.words; ++j) {
+            const int u = 64 * j + lane;
+            const bool isB = u < n && fcnt[u] != 0;
+            const uint64_t mb = __ballot(isB);
+            if (!mb) continue;
+            if (lane == 0) atomicOr((unsigned long long *)&sb[j], (unsigned long long)mb);
+            if (isB) {
+                const NodeRec<RMAX> ru = G[u];
+                const uint32_t nbm = (uint32_t)(ru.meta >> kMetaNbrShift) & 0xffffu;
+#pragma unroll
+                for (int i = 0; i < RMAX; ++i)
+                    if ((nbm >> i) & 1u) {
+                        const int w = ring_entry<RMAX>(ru.ring, i);
+                        atomicOr((uint32_t *)sb + (w >> 5), 1u << (w & 31));
+                    }
+            }
+        }
+        compiler_fence();
+        band_count();
+    };
+    if constexpr (BAND) band_count();
 #ifdef FC_PHASE_PROF
     {  // slot 20: the wave's SIMD (XCC_ID . HW_ID[15:4], as deal_chain keys it)
         uint32_t hw, xcc;
@@ -274,6 +324,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // this lane's non-hit draw in round r (offset 64 r + lane): node | (slots drawn before it
         // << 16), -1: none.  "slot s precedes the draw" is then s < rv >> 16.
         int rv[NSUB];
+        // BAND: lane l < words holds the members of S in the words below l (the rank search's keys)
+        int bpre = 0x7fffffff;
+        if constexpr (BAND) {
+            const int cw = lane < p.words ? (int)__popcll(sb[lane]) : 0;
+            const int inc = wave_scan_incl(cw);
+            if (lane < p.words) bpre = inc - cw;
+        }
 #pragma unroll
         for (int r = 0; r < NSUB; ++r) {
             rv[r] = -1;
@@ -297,9 +354,29 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 w = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
 #endif
             }
-            const uint64_t m = (uint64_t)w.x0 * (uint64_t)(uint32_t)n;
-            const int vd = (int)(m >> 32);
-            const bool okd = inrange && (uint32_t)m >= p.lemire_thresh;
+            int vd;
+            bool okd;
+            if constexpr (BAND) {
+                // exact Lemire over |S|, then the idx-th member of S: the word by a binary search
+                // over the lanes' prefix counts, the bit by popcount halvings
+                const uint64_t m = (uint64_t)w.x0 * (uint64_t)nS;
+                const int idx = (int)(m >> 32);
+                okd = inrange && (uint32_t)m >= thrS;
+                int bw = 0, bb = 0;
+                for (int st2 = p.band_step0; st2 >= 1; st2 >>= 1) {
+                    const int cand = bw + st2;
+                    const int pc = __builtin_amdgcn_ds_bpermute(cand << 2, bpre);
+                    if (pc <= idx) {
+                        bw = cand;
+                        bb = pc;
+                    }
+                }
+                vd = 64 * bw + select_bit64(sb[bw], idx - bb);
+            } else {
+                const uint64_t m = (uint64_t)w.x0 * (uint64_t)(uint32_t)n;
+                vd = (int)(m >> 32);
+                okd = inrange && (uint32_t)m >= p.lemire_thresh;
+            }
             const bool hitd = okd && fcnt[vd] != 0;
             const uint64_t hm = __ballot(hitd);
             const int sp = nh + count_below(hm);
@@ -376,6 +453,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         int end = ns, pos = 0;
         int trunc_off = gen;  // first draw offset not consumed by this batch
         bool target_hit = false;
+        bool rebuild = false;  // BAND: a committed flip put a node outside S into b_nodes
         const int cut0 = cut, nb0 = nb, rem0 = rem;
         const int64_t steps0 = steps;
         const int last_flip0 = last_flip;
@@ -400,7 +478,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             if (st & LF_WROTE) {
                 smark[v] = 0xff;
 #pragma unroll
-                for (int i = 0; i < RMAX; ++i) *(((nbr >> i) & 1u) ? &nmark[cell[i]] : dum) = 0xff;
+                for (int i = 0; i < RMAX; ++i) FC_ST(((nbr >> i) & 1u), nmark[cell[i]], 0xff);
             }
             st &= ~LF_WROTE;
             compiler_fence();
@@ -587,10 +665,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     for (int i = 0; i < RMAX; ++i) mn[i] = 0xff;
                     for (;;) {
                         FC_PROF(21, 1);
-                        *((need && ms > lane) ? &smark[v] : dum) = (uint8_t)lane;
+                        FC_ST(need && ms > lane, smark[v], lane);
 #pragma unroll
                         for (int i = 0; i < RMAX; ++i)
-                            *((need && ((nbr >> i) & 1u) && mn[i] > lane) ? &nmark[cell[i]] : dum) = (uint8_t)lane;
+                            FC_ST(need && ((nbr >> i) & 1u) && mn[i] > lane, nmark[cell[i]], lane);
                         compiler_fence();
                         ms = smark[v];
 #pragma unroll
@@ -642,7 +720,33 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 }
                 FC_STAMP(t_cf);
                 FC_PROF(19, t_cf - t_it1);
-                const int ce = min(sg, x);  // commit lanes [pos, ce)
+                int ce = min(sg, x);  // commit lanes [pos, ce)
+                bool seg_out = false;
+                if constexpr (BAND) {
+                    // the first candidate whose flip puts a neighbour outside S into b_nodes is the
+                    // segment's last commit (later draws map through the rebuilt S).  Inside a
+                    // segment no two flips share a neighbour (beta), so the counts read here are
+                    // each flip's own sequential view
+                    const uint64_t K0 = K & bits_below(ce);
+                    if (K0) {
+                        bool out = false;
+                        if ((K0 >> lane) & 1ull) {
+#pragma unroll
+                            for (int i = 0; i < RMAX; ++i) {
+                                const int u = cell[i];
+                                const uint32_t oc = fcnt[u];
+                                const uint64_t swd = sb[u >> 6];
+                                out |= ((nbr & inA) >> i & 1u) && oc == 0u && !((swd >> (u & 63)) & 1ull);
+                            }
+                        }
+                        const uint64_t IV = __ballot(out);
+                        if (IV) {
+                            ce = __builtin_ctzll(IV) + 1;
+                            seg_out = true;
+                            if (ce < sg) last_step = false;
+                        }
+                    }
+                }
                 if (x < sg) last_step = false;
                 if (prop && lane < ce) st |= valid1 ? (cand1 ? (ST_VS | ST_AC) : ST_VS) : (ok1 ? ST_IP : ST_IC);
                 rem -= __popcll(VAL & bits_below(ce));
@@ -661,11 +765,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     for (int i = 0; i < RMAX; ++i) {
                         const bool nb_i = me && ((nbr >> i) & 1u);
                         const uint32_t up = (inA >> i) & 1u, dn = (tmask >> i) & 1u;  // dlt = up - dn
-                        *(nb_i ? &fcnt[cell[i]] : dum) = (uint8_t)(oldc[i] + (int)up - (int)dn);
+                        FC_ST(nb_i, fcnt[cell[i]], oldc[i] + (int)up - (int)dn);
                         dnb += nb_i ? (int)(up & (uint32_t)(oldc[i] == 0)) - (int)(dn & (uint32_t)(oldc[i] == 1)) : 0;
                     }
-                    *(me ? (uint8_t *)&a[v] : dum) = (uint8_t)(1 - av);
-                    *(me ? &fcnt[v] : dum) = (uint8_t)nA;
+                    FC_ST(me, *(uint8_t *)&a[v], 1 - av);
+                    FC_ST(me, fcnt[v], nA);
                     const int pkd = me ? ((delta + 32) | ((dnb + 32) << 16)) : 0;
                     const int S = wave_scan_incl(pkd);
                     const int cntA = count_below(AP) + 1;
@@ -687,15 +791,21 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 if (st & LF_WROTE) {  // clear this pass's marks: the next pass starts clean
                     smark[v] = 0xff;
 #pragma unroll
-                    for (int i = 0; i < RMAX; ++i) *(((nbr >> i) & 1u) ? &nmark[cell[i]] : dum) = 0xff;
+                    for (int i = 0; i < RMAX; ++i) FC_ST(((nbr >> i) & 1u), nmark[cell[i]], 0xff);
                     st &= ~LF_WROTE;
                 }
                 FC_STAMP(t_sg1);
                 FC_PROF(11, t_sg1 - t_it1);
                 pos = ce;
+                if (BAND && seg_out) rebuild = true;
                 if (last_step) {
                     end = pos;
                     target_hit = true;
+                    break;
+                }
+                if (BAND && seg_out) {
+                    end = pos;
+                    trunc_off = rl32(off_l, pos - 1) + 1;
                     break;
                 }
                 if (pos >= end) break;
@@ -750,12 +860,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const bool is_nbr = lane < RMAX && ((nbrf >> lane) & 1u);
             // foreign-neighbour counts: u sees v leave A (+1 if u in A) and join t (-1 if u in t)
             const int dlt = (int)((inAf >> lane) & 1u) - (int)((tmf >> lane) & 1u);
-            bool enter = false, leave = false;
+            bool enter = false, leave = false, outS = false;
             if (is_nbr) {
                 const int old = fcnt[my_e];
+                const uint64_t swd = BAND ? sb[my_e >> 6] : 0ull;
                 fcnt[my_e] = (uint8_t)(old + dlt);
                 enter = dlt > 0 && old == 0;
                 leave = dlt < 0 && old == 1;
+                outS = BAND && enter && !((swd >> (my_e & 63)) & 1ull);
             }
             if (lane == 0) {
                 a[vf] = (int8_t)(1 - Af);
@@ -817,9 +929,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             FC_STAMP(t_ap1);
             FC_PROF(10, t_ap1 - t_ap0);
             pos = f + 1;
+            const bool f_out = BAND && __ballot(outS) != 0ull;  // S is rebuilt after this flip
+            if (f_out) rebuild = true;
             if (rem == 0) {
                 end = pos;
                 target_hit = true;
+                break;
+            }
+            if (f_out) {
+                end = pos;
+                trunc_off = rl32(off_l, f) + 1;
                 break;
             }
             if (aff && pos < end) reeval(pos, vf, eqm);
@@ -827,7 +946,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         if (st & LF_WROTE) {  // clear this lane's marks for the next batch
             smark[v] = 0xff;
 #pragma unroll
-            for (int i = 0; i < RMAX; ++i) *(((nbr >> i) & 1u) ? &nmark[cell[i]] : dum) = 0xff;
+            for (int i = 0; i < RMAX; ++i) FC_ST(((nbr >> i) & 1u), nmark[cell[i]], 0xff);
         }
         compiler_fence();
         steps = steps0 + (rem0 - rem);
@@ -1020,6 +1139,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             if (trunc_off < consumed) consumed = trunc_off;
         }
         draw += (uint64_t)consumed;
+        if constexpr (BAND) {
+            if (rebuild) {
+                FC_STAMP(t_rb0);
+                band_rebuild();
+                FC_STAMP(t_rb1);
+                FC_PROF(22, 1);
+                FC_PROF(23, t_rb1 - t_rb0);
+            }
+        }
+        FC_PROF(24, ns);
         compiler_fence();
         FC_STAMP(t_e);
         FC_PROF(4, t_e - t_d);
@@ -1052,6 +1181,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             ga[i] = ((const uint4 *)a)[i];
             gf[i] = ((const uint4 *)fcnt)[i];
         }
+        if (BAND && lane < p.words) p.sbits[(size_t)c * p.words + lane] = sb[lane];
     }
     const int64_t cnt_prop = n_prop, cnt_acc = n_acc, cnt_ic = n_ic, cnt_ip = n_ip;  // already wave totals
 #pragma unroll
@@ -1109,15 +1239,20 @@ int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_
     const bool xtra = p.tape || p.trace || p.variant;
     // no search code when the run rule decides every proposal (all nodes exact, no forced search)
     const bool search = !p.all_exact || (p.flags & FC_FLAG_FORCE_BFS);
-#define FC_LAUNCH2(R, S, F, X, Y)                                                                       \
-    do {                                                                                                \
-        if (lds > 65536)                                                                                \
-            (void)hipFuncSetAttribute((const void *)flip2_kernel<R, S, F, X, Y>,                        \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
-        if (name)                                                                                       \
-            snprintf(name, name_cap, "fc::flip2_kernel<%d, %d, %s, %s, %s>", R, S, F ? "true" : "false", \
-                     X ? "true" : "false", Y ? "true" : "false");                                      \
-        hipLaunchKernelGGL((flip2_kernel<R, S, F, X, Y>), grid, block, lds, s, p);                      \
+#define FC_LAUNCH2B(R, S, F, X, Y, B)                                                                      \
+    do {                                                                                                    \
+        if (lds > 65536)                                                                                    \
+            (void)hipFuncSetAttribute((const void *)flip2_kernel<R, S, F, X, Y, B>,                         \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
+        if (name)                                                                                           \
+            snprintf(name, name_cap, "fc::flip2_kernel<%d, %d, %s, %s, %s, %s>", R, S, F ? "true" : "false", \
+                     X ? "true" : "false", Y ? "true" : "false", B ? "true" : "false");                    \
+        hipLaunchKernelGGL((flip2_kernel<R, S, F, X, Y, B>), grid, block, lds, s, p);                       \
+    } while (0)
+#define FC_LAUNCH2(R, S, F, X, Y)                        \
+    do {                                                 \
+        if (p.band) FC_LAUNCH2B(R, S, F, X, Y, true);    \
+        else FC_LAUNCH2B(R, S, F, X, Y, false);          \
     } while (0)
 #define FC_SEARCH2(R, S, F, Y)                    \
     do {                                          \
@@ -1148,6 +1283,7 @@ int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_
 #undef FC_FULL2
 #undef FC_SEARCH2
 #undef FC_LAUNCH2
+#undef FC_LAUNCH2B
     return (int)hipGetLastError();
 }
 

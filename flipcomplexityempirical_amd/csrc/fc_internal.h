@@ -153,6 +153,11 @@ struct KParams {
     uint32_t *deal;             // [kDealKeys + 4]: arrivals per SIMD key, claims per quarter (zeroed per launch)
     const uint32_t *order;      // [n_chains] chain ids, slowest first (null: no dealing)
     uint32_t *ctime;            // [n_chains] draws each chain took in its last launch (the dealing key)
+    // k = 2 band stream (FC_STREAM_BAND): per chain the band S = b_nodes + neighbours as a
+    // bitmap of `words` u64; a draw selects the i-th member (fc_flip2.hip)
+    int32_t band;
+    int32_t band_step0;         // largest power of two below `words` (rank search over the words)
+    uint64_t *sbits;            // [n_chains * words]
 };
 
 // chain dealing: SIMD keys are XCC_ID[2:0] . HW_ID[15:4] (SIMD, pipe, CU, SH, SE)
@@ -162,7 +167,7 @@ constexpr int kDealKeys = 1 << 15;
 // slots: 0 loop total, 1 draws, 2 evaluate, 3 commit, 4 bookkeeping, 5 batches,
 //        6 commit-loop iterations, 7 applied flips; k = 2 commit detail: 8 verdicts,
 //        9 one-event classify, 10 one-event apply, 11 segment-parallel, 12 segments
-constexpr int kProfSlots = 24;
+constexpr int kProfSlots = 28;
 // k = 2 lean kernel: accepted states queued for their geometric wait (fc_flip2.hip wait_flush)
 constexpr int kWaitQ = 64;
 // k > 2 kernel: 32 entries, so that sec11 chains keep four waves per SIMD in 160 KB of LDS

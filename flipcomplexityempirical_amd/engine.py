@@ -137,6 +137,9 @@ class RunConfig:
     # Keys: nsub, hit_stop, par_min, wait_queue, chains_per_block, prio_div (3), prio_th (3),
     # search_waves, deal.
     tune: Optional[Dict[str, object]] = None
+    # k = 2 node stream (fc_params.stream): "node" draws over all n nodes, "band" over the band
+    # S = b_nodes + neighbours; the chain's law is the same, the trajectory not
+    stream: str = "node"
 
 
 TUNE_KEYS = ("nsub", "hit_stop", "par_min", "wait_queue", "chains_per_block", "prio_div", "prio_th",
@@ -202,6 +205,9 @@ class FlipRun:
                     hit_hi=int(cfg.hit_hi), event_cap=int(cfg.event_cap), accept=int(cfg.accept),
                     con_valid=int(cfg.con_valid), con_accept=int(cfg.con_accept), beta=float(cfg.beta))
         prm.chain_pop_bounds = _p(self._pop_bounds, ctypes.c_int64)
+        if cfg.stream not in ("node", "band"):
+            raise ValueError(f"stream must be 'node' or 'band', not {cfg.stream!r}")
+        prm.stream = _lib.STREAM_BAND if cfg.stream == "band" else _lib.STREAM_NODE
         self._frozen = np.ascontiguousarray(list(cfg.frozen), dtype=np.int32)
         prm.frozen = _p(self._frozen, ctypes.c_int32)
         prm.n_frozen = int(self._frozen.size)
@@ -459,7 +465,7 @@ class FlipRun:
         return {"slope": slope[sel], "angle": angle[sel], "n_cut": ncut[sel], "len": ln[sel]}
 
     def frame_series_changes(self, frame, c0: int = 0, nc: Optional[int] = None,
-                             out: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
+                             out: Optional[Dict[str, np.ndarray]] = None, query: bool = False) -> Dict[str, np.ndarray]:
         """Change points of the slope / angle series of chains ``c0 .. c0 + nc - 1``
         (``fc_run_frame_series_changes``): ``offsets`` [nc + 1] and flat ``t`` (int64), ``slope``,
         ``angle`` (float64); chain ``c0 + i`` owns entries ``offsets[i]:offsets[i + 1]``, each
@@ -467,7 +473,8 @@ class FlipRun:
         plots draw (``grid_chain_sec11.py:476-484``); :meth:`changes_to_yields` expands one chain
         to its per-yield lists (``:382,394``).  ``out`` (optional): C-contiguous int64 / float64 /
         float64 buffers ``t`` / ``slope`` / ``angle`` to fill (e.g. pinned with
-        :func:`pin_host`); used when large enough, the result then holds views of them."""
+        :func:`pin_host`); used when large enough, the result then holds views of them.
+        ``query``: only the offsets (sizing buffers)."""
         nc = self.n_chains - c0 if nc is None else int(nc)
         L = _lib.load()
         eu = np.ascontiguousarray(frame.eu, dtype=np.int32)
@@ -476,20 +483,31 @@ class FlipRun:
         off = np.zeros(nc + 1, dtype=np.int64)
         args = (self.handle, int(c0), nc, int(eu.size), _p(eu, ctypes.c_int32), _p(ev, ctypes.c_int32),
                 _p(mid, ctypes.c_double), float(frame.center[0]), float(frame.center[1]))
-        check(L.fc_run_frame_series_changes(*args, 0, _p(off, ctypes.c_int64), _P(ctypes.c_int64)(),
-                                            _P(ctypes.c_double)(), _P(ctypes.c_double)()), "fc_run_frame_series_changes")
-        total = int(off[-1])
-        bufs = None
-        if out is not None:
+        if out is not None and not query:
             for key, dt in (("t", np.int64), ("slope", np.float64), ("angle", np.float64)):
                 b = out.get(key)
                 if not isinstance(b, np.ndarray) or b.dtype != dt or not b.flags.c_contiguous or not b.flags.writeable:
                     raise ValueError(f"frame_series_changes: out[{key!r}] must be a writeable C-contiguous "
                                      f"{np.dtype(dt)} array")
-            if min(out[key].size for key in ("t", "slope", "angle")) >= total:
-                bufs = {key: out[key].reshape(-1)[:total] for key in ("t", "slope", "angle")}
-        if bufs is None:
-            bufs = {"t": np.empty(total, dtype=np.int64), "slope": np.empty(total), "angle": np.empty(total)}
+            # one call: count, offsets, write and copy into the caller's buffers when they hold
+            # every change point (the offsets come back either way)
+            cap = min(out[key].size for key in ("t", "slope", "angle"))
+            flat = {key: out[key].reshape(-1) for key in ("t", "slope", "angle")}
+            rc = L.fc_run_frame_series_changes(*args, cap, _p(off, ctypes.c_int64), _p(flat["t"], ctypes.c_int64),
+                                               _p(flat["slope"], ctypes.c_double), _p(flat["angle"], ctypes.c_double))
+            total = int(off[-1])
+            if rc == 0:
+                return {"offsets": off, **{key: b[:total] for key, b in flat.items()}}
+            if total <= cap:
+                check(rc, "fc_run_frame_series_changes")
+        else:
+            check(L.fc_run_frame_series_changes(*args, 0, _p(off, ctypes.c_int64), _P(ctypes.c_int64)(),
+                                                _P(ctypes.c_double)(), _P(ctypes.c_double)()),
+                  "fc_run_frame_series_changes")
+            total = int(off[-1])
+            if query:
+                return {"offsets": off}
+        bufs = {"t": np.empty(total, dtype=np.int64), "slope": np.empty(total), "angle": np.empty(total)}
         check(L.fc_run_frame_series_changes(*args, total, _p(off, ctypes.c_int64), _p(bufs["t"], ctypes.c_int64),
                                             _p(bufs["slope"], ctypes.c_double), _p(bufs["angle"], ctypes.c_double)),
               "fc_run_frame_series_changes")

@@ -39,7 +39,7 @@ extern "C" {
 
 /* fc_params.struct_size / abi_version: a caller built against another layout of fc_params is
  * rejected (FC_ERR_ARG) instead of read past.  Bumped whenever fc_params changes.           */
-#define FC_ABI_VERSION 3u
+#define FC_ABI_VERSION 4u
 
 /* fc_graph_create flags */
 #define FC_GRAPH_NO_EXACT 0x1u   /* never trust the planar local contiguity rule            */
@@ -168,7 +168,18 @@ typedef struct fc_params {
      * whole sweep is one run.                                                                   */
     const int64_t *chain_pop_bounds; /* [2 * n_chains]: chain c's inclusive (pop_lo, pop_hi), or
                                         NULL for pop_lo / pop_hi                                 */
+    /* Node stream of k = 2 runs.  Both are rejection sampling of the reference's
+     * random.choice(list(b_nodes)) (grid_chain_sec11.py:143), so the chain's law is the same;
+     * the trajectories differ.  FC_STREAM_NODE (0): a draw picks one of all n nodes.
+     * FC_STREAM_BAND: a draw picks the i-th node (ascending) of the band S = b_nodes plus their
+     * neighbours, which the chain keeps lazily: after an accepted flip that puts a node outside
+     * S into b_nodes, S is rebuilt from that state.  Short boundaries then waste few draws.
+     * k = 2, n <= 4096, no replay tape; oracle: fr_params.stream                               */
+    int32_t stream;
 } fc_params;
+
+#define FC_STREAM_NODE 0
+#define FC_STREAM_BAND 1
 
 /* Zero *p, then set struct_size / abi_version and the defaults a zeroed struct does not give:
  * base 1, pop bounds [0, INT32_MAX], hitting-time window off.  FC_ERR_ARG when struct_size is
@@ -338,7 +349,10 @@ int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, cons
  * (the last up to the current yield); the first entry is the window start, and every later one
  * is an event whose slope or angle differs (bitwise) from the previous entry's.  offsets
  * [nc + 1] is always filled; with t, slope and angle all NULL the call only sizes the output,
- * otherwise cap (entries per output array) must be >= offsets[nc] (FC_ERR_ARG).  k = 2 only. */
+ * otherwise cap (entries per output array) must be >= offsets[nc] (FC_ERR_ARG, offsets still
+ * filled, so a caller with buffers of a guessed size calls once and only re-calls on a miss).
+ * The run keeps the device tables and outputs between calls (one call per launch of a driver
+ * loop costs two kernel passes, one small round trip for the offsets and three copies).  k = 2. */
 int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *frame_u,
                                 const int32_t *frame_v, const double *mid_xy, double cx, double cy, int64_t cap,
                                 int64_t *offsets, int64_t *t, double *slope, double *angle);

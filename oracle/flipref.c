@@ -244,11 +244,29 @@ static int32_t nb_after_flip(ctx_t *c, int32_t v, int8_t T) {
     return c->nb + after - before;
 }
 
+/* Band stream: S = b_nodes and their neighbours, as an ascending node list (the rank a draw
+ * selects) and a membership flag per node.  Returns |S|. */
+static int32_t band_build(const ctx_t *c, uint8_t *ins, int32_t *slist) {
+    const fr_params *p = c->p;
+    memset(ins, 0, (size_t)p->n);
+    for (int32_t u = 0; u < p->n; ++u) {
+        if (!in_boundary(c, u)) continue;
+        ins[u] = 1;
+        for (int32_t j = p->row_ptr[u]; j < p->row_ptr[u + 1]; ++j) ins[p->col_idx[j]] = 1;
+    }
+    int32_t ns = 0;
+    for (int32_t u = 0; u < p->n; ++u)
+        if (ins[u]) slist[ns++] = u;
+    return ns;
+}
+
 int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outputs *o) {
     if (!p || !init_assign || !st || p->n <= 0 || p->k < 2 || p->k > 64 || !p->row_ptr || !p->col_idx || !p->pop)
         return -2;
     if (p->proposal == FR_PROPOSE_BI_SIGN && p->k != 2) return -2;
     if (p->proposal != FR_PROPOSE_BI_SIGN && p->proposal != FR_PROPOSE_PAIR) return -2;
+    if (p->stream != FR_STREAM_NODE && p->stream != FR_STREAM_BAND) return -2;
+    if (p->stream == FR_STREAM_BAND && (p->k != 2 || p->tape)) return -2;
     if (o && o->num_flips && (!o->part_sum || !o->last_flipped || !p->labels)) return -2;
     if (o && o->occupancy && (!o->flip_count || !o->last_accept || !p->labels)) return -2;
     const int32_t n = p->n;
@@ -257,6 +275,8 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
 
     ctx_t c; memset(&c, 0, sizeof c);
     int32_t *nf = NULL, nfh[65];  /* PAIR: foreign districts per node, and their histogram */
+    uint8_t *ins = NULL;          /* band stream: membership of S, and S ascending          */
+    int32_t *slist = NULL, ns = 0;
     memset(nfh, 0, sizeof nfh);
     c.p = p;
     c.a = (int8_t *)malloc((size_t)n);
@@ -329,6 +349,14 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
         }
     }
     uint32_t wthresh = (uint32_t)((0x100000000ull) % (uint64_t)wcap);
+    uint32_t sthresh = 0;
+    if (p->stream == FR_STREAM_BAND) {
+        ins = (uint8_t *)malloc((size_t)n);
+        slist = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+        if (!ins || !slist) { rc = -2; goto done; }
+        ns = band_build(&c, ins, slist);
+        sthresh = (uint32_t)((0x100000000ull) % (uint64_t)ns);
+    }
     int64_t d = 0;
     while (st->steps < p->n_steps) {
         if ((p->max_draws > 0 && st->draws >= p->max_draws) || (p->tape && d >= p->tape_draws)) {
@@ -338,9 +366,16 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
         draw_words(p, d, 0, w);
         const int64_t draw = d++;
         st->draws += 1;
-        const uint64_t m = (uint64_t)w[0] * (uint64_t)n;
-        if ((uint32_t)m < thresh) continue;                   /* Lemire: exact uniform node */
-        const int32_t v = (int32_t)(m >> 32);
+        int32_t v;
+        if (ins) {                                              /* band: i-th node of S     */
+            const uint64_t m = (uint64_t)w[0] * (uint64_t)ns;
+            if ((uint32_t)m < sthresh) continue;
+            v = slist[m >> 32];
+        } else {
+            const uint64_t m = (uint64_t)w[0] * (uint64_t)n;
+            if ((uint32_t)m < thresh) continue;               /* Lemire: exact uniform node */
+            v = (int32_t)(m >> 32);
+        }
         if (!in_boundary(&c, v)) continue;                      /* not in b_nodes_bi        */
         const int8_t A = c.a[v];
         int8_t T;
@@ -433,6 +468,15 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
                     wthresh = (uint32_t)((0x100000000ull) % (uint64_t)wcap);
                 }
             }
+            if (ins) {  /* a neighbour entering b_nodes outside S: S is rebuilt from this state */
+                int out = 0;
+                for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1] && !out; ++j)
+                    out = !ins[p->col_idx[j]] && in_boundary(&c, p->col_idx[j]);
+                if (out) {
+                    ns = band_build(&c, ins, slist);
+                    sthresh = (uint32_t)((0x100000000ull) % (uint64_t)ns);
+                }
+            }
             st->wait_cur = geom_wait(p, draw, 1, c.nb);
             if (o && o->occupancy) { o->flip_count[v] += 1; o->last_accept[v] = st->steps; }
         }
@@ -456,6 +500,7 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
     }
 done:
     free(nf);
+    free(ins); free(slist);
     free(c.a); free(c.pops); free(c.stamp); free(c.queue); free(c.eu); free(c.ev);
     return rc;
 }

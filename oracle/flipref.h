@@ -15,7 +15,8 @@
  * Random stream (the shared canonical spec, see DESIGN.md "Random stream"): draw d of
  * chain c uses Philox4x32-10(ctr = (lo32 d, hi32 d, c, 0), key = (lo32 seed, hi32 seed)).
  * Node = Lemire multiply-shift of word 0 over N (exact: reject low < 2^32 mod N); a draw
- * whose node is not a boundary node is not a proposal.  Acceptance U53 = CPython random()
+ * whose node is not a boundary node is not a proposal.  Band stream (FR_STREAM_BAND): the
+ * same map over |S| picks the i-th node of the band S in ascending order instead.  Acceptance U53 = CPython random()
  * from words (1, 2).  The geometric wait of the state created by draw d uses purpose 1,
  * the initial state's purpose 2 at d = 0; U53 from words (0, 1).
  * A tape (6 u32 per draw: the 4 proposal words then the 2 geometric words) may replace
@@ -94,7 +95,15 @@ typedef struct fr_params {
     /* node-tape replay: the two words of the initial state's geometric
      * wait (numpy's draw in the reference, geom_wait :147-148); NULL = Philox purpose 2   */
     const uint32_t *wait0_words;
+    /* node stream (k = 2 BI_SIGN): FR_STREAM_NODE draws the node uniformly over all N nodes;
+     * FR_STREAM_BAND uniformly over the band S, a superset of b_nodes kept lazily: S = b_nodes
+     * plus their neighbours, recomputed after an accepted flip only when a node enters b_nodes
+     * outside S.  Either is rejection sampling of random.choice(b_nodes)   */
+    int32_t stream;
 } fr_params;
+
+#define FR_STREAM_NODE 0
+#define FR_STREAM_BAND 1
 
 #define FR_ACCEPT_CUT 0        /* cut_accept                          :171-179 */
 #define FR_ACCEPT_UNIFORM 1    /* uniform_accept                      :159-165 */

@@ -112,7 +112,8 @@ class FrParams(ctypes.Structure):
                 ("log1mp", _P(ctypes.c_double)), ("proposal", ctypes.c_int32), ("wmax", ctypes.c_int32),
                 ("accept", ctypes.c_int32), ("con_valid", ctypes.c_uint32), ("con_accept", ctypes.c_uint32),
                 ("beta", ctypes.c_double), ("boundary", _P(ctypes.c_uint8)), ("pinned", _P(ctypes.c_int32)),
-                ("n_pinned", ctypes.c_int32), ("wait0_words", _P(ctypes.c_uint32))]
+                ("n_pinned", ctypes.c_int32), ("wait0_words", _P(ctypes.c_uint32)),
+                ("stream", ctypes.c_int32)]
 
 
 ACCEPT_CUT, ACCEPT_UNIFORM, ACCEPT_ANNEAL = 0, 1, 2
@@ -120,6 +121,7 @@ CON_CONTIG, CON_POP, CON_BOUNDARY, CON_FIXED, CON_EMPTY = 1, 2, 4, 8, 0x100
 
 
 PROPOSE_BI_SIGN, PROPOSE_PAIR = 0, 1
+STREAM_NODE, STREAM_BAND = 0, 1  # flipref.h FR_STREAM_*
 
 
 class FrOutputs(ctypes.Structure):
@@ -198,7 +200,8 @@ class CRef:
             want_edges: bool = False, want_flips: bool = False, proposal: int = 0, wmax: int = 0,
             accept: int = 0, con_valid: int = 0, con_accept: int = 0, beta: float = 0.0,
             boundary: Optional[np.ndarray] = None, pinned: Optional[np.ndarray] = None,
-            wait0_words: Optional[np.ndarray] = None, want_exact_flips: bool = False) -> Dict:
+            wait0_words: Optional[np.ndarray] = None, want_exact_flips: bool = False,
+            stream: int = STREAM_NODE) -> Dict:
         n, E = spec.n, spec.n_edges
         row_ptr = np.ascontiguousarray(spec.row_ptr, dtype=np.int32)
         col_idx = np.ascontiguousarray(spec.col_idx, dtype=np.int32)
@@ -221,7 +224,7 @@ class CRef:
                      proposal=int(proposal), wmax=int(wmax), accept=int(accept), con_valid=int(con_valid),
                      con_accept=int(con_accept), beta=float(beta), boundary=_ptr(bnd, ctypes.c_uint8),
                      pinned=_ptr(pin, ctypes.c_int32), n_pinned=0 if pin is None else pin.size // 2,
-                     wait0_words=_ptr(w0, ctypes.c_uint32))
+                     wait0_words=_ptr(w0, ctypes.c_uint32), stream=int(stream))
         trace = np.zeros(trace_cap, dtype=RECORD_DTYPE) if trace_cap else None
         final = np.zeros(n, dtype=np.int8)
         cut_hist = np.zeros(E + 1, dtype=np.int64) if want_hist else None
@@ -381,7 +384,7 @@ class GcFaithfulChain:
 
     def __init__(self, spec, plan: Dict, *, base: float, pop_bounds, seed: int, chain_id: int,
                  log1mp: Optional[np.ndarray] = None, tape: Optional[np.ndarray] = None,
-                 pair: bool = False, wmax: int = 0):
+                 pair: bool = False, wmax: int = 0, band: bool = False):
         self.spec = spec
         self.g = spec.nx_graph
         self.base = base
@@ -404,8 +407,22 @@ class GcFaithfulChain:
         self.stats = dict(steps=0, proposals=0, draws=0, accepted=0, inv_contig=0, inv_pop=0,
                           sum_cut=0, sum_nb=0, sum_wait=0)
         self.trace = []
+        # band stream (flipref.h FR_STREAM_BAND): nodes drawn over S = b_nodes + neighbours,
+        # ascending, rebuilt only when a node enters b_nodes outside S
+        self.band = band
+        if band:
+            self._band_build()
         self.wait = self._geom(0, 2)
         self._yield()
+
+    def _band_build(self):
+        idx = self.spec.index
+        S = set()
+        for x in self.state["b_nodes"]:
+            S.add(idx[x])
+            S.update(idx[y] for y in self.g.neighbors(x))
+        self.band_set = S
+        self.band_list = sorted(S)
 
     def _words(self, d, purpose):
         if self.tape is not None and purpose != 2:
@@ -448,10 +465,11 @@ class GcFaithfulChain:
             w = self._words(draw, 0)
             self.d += 1
             self.stats["draws"] += 1
-            m = w[0] * self.n
-            if (m & 0xFFFFFFFF) < self.thresh:
+            ns = len(self.band_list) if self.band else self.n
+            m = w[0] * ns
+            if (m & 0xFFFFFFFF) < (1 << 32) % ns:
                 continue
-            node = self.spec.nodes[m >> 32]
+            node = self.spec.nodes[self.band_list[m >> 32] if self.band else m >> 32]
             s = self.state
             if node not in s["b_nodes"]:
                 continue
@@ -484,6 +502,8 @@ class GcFaithfulChain:
             if acc:
                 self.state = proposal
                 self.stats["accepted"] += 1
+                if self.band and any(self.spec.index[x] not in self.band_set for x in proposal["b_nodes"]):
+                    self._band_build()
                 self.wait = self._geom(draw, 1)
             self._yield()
             cur = self.state
@@ -595,6 +615,8 @@ class NativeRngChain(GcFaithfulChain):
             if acc:
                 self.state = proposal
                 self.stats["accepted"] += 1
+                if self.band and any(self.spec.index[x] not in self.band_set for x in proposal["b_nodes"]):
+                    self._band_build()
                 self.wait = self._geom(0, 1)
                 if self.record:
                     words[4], words[5] = self._geom_words

@@ -99,8 +99,11 @@ def shape_from_events(spec, frame, a0, events, T):
     return mean, vals[-1]
 
 
+@pytest.mark.parametrize("stream", [0, 1], ids=["node", "band"])
 @pytest.mark.parametrize("cfg,bi", CASES)
-def test_canonical_oracle_matches_native_rng(cref, cfg, bi):
+def test_canonical_oracle_matches_native_rng(cref, cfg, bi, stream):
+    """Both node streams (flipref.h FR_STREAM_NODE / FR_STREAM_BAND) sample the reference's
+    chain: uniform over b_nodes, whatever superset the draws range over."""
     fix = fixture(cfg)
     T, base = int(fix["T"]), float(fix["bases"][bi])
     spec, a0, lo, hi = setup(cfg)
@@ -109,7 +112,8 @@ def test_canonical_oracle_matches_native_rng(cref, cfg, bi):
     finals, waits, sc, sn, am, ae = [], [], [], [], [], []
     for c in range(600 if T <= 2000 else 150):
         r = cref.run(spec, a0, base=base, pop_lo=lo, pop_hi=hi, seed=0xD15, chain_id=c, n_steps=T,
-                     log1mp=G.log1mp_table(spec.n, 2), trace_cap=64 * T if frame is not None else 0)
+                     log1mp=G.log1mp_table(spec.n, 2), trace_cap=64 * T if frame is not None else 0,
+                     stream=stream)
         finals.append(r["final"])
         waits.append(r["stats"]["wait_cur"])
         sc.append(r["stats"]["sum_cut"])
@@ -123,4 +127,4 @@ def test_canonical_oracle_matches_native_rng(cref, cfg, bi):
     got = summarize(spec, finals, waits, sc, sn, T)
     if frame is not None:
         got["angle_mean"], got["angle_end"] = np.asarray(am), np.asarray(ae)
-    assert_same_distribution(fix, bi, got, f"C oracle {cfg}")
+    assert_same_distribution(fix, bi, got, f"C oracle {cfg} stream {stream}")

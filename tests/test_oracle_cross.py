@@ -206,3 +206,35 @@ def test_c_oracle_pair_slot_bound_long_chain(cref):
     fixed = cref.run(spec, a0, base=1.0, pop_lo=ilo, pop_hi=ihi, seed=9, chain_id=3, n_steps=steps, k=k,
                      labels=labels, log1mp=l1, proposal=1, wmax=k - 1)
     assert fixed["stats"]["draws"] > r["stats"]["draws"]  # the fixed bound wastes more slot draws
+
+
+@pytest.mark.parametrize("base,al,steps", [(1.0, 0, 300), (G.SEC11_MU, 1, 1500), (10, 2, 2000)])
+def test_band_stream_c_equals_gc_faithful(cref, sec11, base, al, steps):
+    """The band stream (nodes drawn over S = b_nodes + neighbours, rebuilt lazily) is the same
+    in both restatements, S rebuilds included."""
+    from oracle.flipref import GcFaithfulChain, STREAM_BAND
+    l1 = G.log1mp_table(sec11.n, 2)
+    plan = G.sec11_plan(al, sec11.nodes)
+    a0 = sec11.assignment_array(plan, [-1, 1])
+    (lo, hi), (ilo, ihi) = G.population_bounds(sec11.n, 2, 0.1)
+    gc = GcFaithfulChain(sec11, plan, base=base, pop_bounds=(lo, hi), seed=5, chain_id=al, log1mp=l1, band=True)
+    rebuilds = 0
+    S = gc.band_set
+    for _ in range(steps):
+        gc.step()
+        rebuilds += gc.band_set is not S
+        S = gc.band_set
+    r = cref.run(sec11, a0, base=base, pop_lo=ilo, pop_hi=ihi, seed=5, chain_id=al, n_steps=steps, log1mp=l1,
+                 trace_cap=200000, stream=STREAM_BAND)
+    gtr = np.array(gc.trace, dtype=np.int64)
+    tr = r["trace"]
+    assert len(tr) == len(gtr)
+    for i, f in enumerate(["draw", "v", "flags", "cut", "nb", "wait"]):
+        assert np.array_equal(tr[f], gtr[:, i]), f
+    assert np.array_equal(gc.assignment_ids(), r["final"])
+    for k in ("steps", "proposals", "draws", "accepted", "sum_cut", "sum_nb", "sum_wait"):
+        assert gc.stats[k] == r["stats"][k], k
+    if base == 10:
+        assert rebuilds >= 2  # the rebuild rule is exercised
+        # short boundary: the band stream wastes far fewer draws than the node stream
+        assert r["stats"]["draws"] < 4 * r["stats"]["proposals"]

@@ -177,3 +177,15 @@ def test_frame_series_changes_equal_per_yield_lists(gpu, sec11, launches):
     finally:
         for b in pinned.values():
             unpin_host(b)
+    # buffers too small: the offsets still come back and the call falls back to fresh arrays
+    small = {"t": np.empty(3, dtype=np.int64), "slope": np.empty(3), "angle": np.empty(3)}
+    ch3 = run.frame_series_changes(frame, c0=2, nc=5, out=small)
+    for key in ("t", "slope", "angle"):
+        assert np.array_equal(ch3[key].view(np.int64), ch[key].view(np.int64)), key
+    # every chain in one call (the run's cached tables and outputs reused), the sizing query
+    q = run.frame_series_changes(frame, query=True)
+    full = run.frame_series_changes(frame)
+    assert np.array_equal(q["offsets"], full["offsets"])
+    lo, hi = int(full["offsets"][2]), int(full["offsets"][7])
+    for key in ("t", "slope", "angle"):
+        assert np.array_equal(full[key][lo:hi].view(np.int64), ch[key].view(np.int64)), key

@@ -14,7 +14,8 @@ inits = np.stack([plans[(c // 10) % 3] for c in range(C)])
 bases = np.asarray([G.SEC11_BASES[c % 10 if B < 0 else B] for c in range(C)])
 (_, _), (lo, hi) = G.population_bounds(1596, 2, 0.1)
 # FC_PROBE_DIAG=<mask> overrides the diagnostics mask (0: no geometric waits)
-cfg = RunConfig(seed=0x5EED0002, pop_lo=lo, pop_hi=hi, tune=parse_tune(os.environ.get('FC_TUNE', '')))
+cfg = RunConfig(seed=0x5EED0002, pop_lo=lo, pop_hi=hi, tune=parse_tune(os.environ.get('FC_TUNE', '')),
+                stream=os.environ.get('FC_STREAM', 'node'))
 if 'FC_PROBE_DIAG' in os.environ: cfg.diag_mask = int(os.environ['FC_PROBE_DIAG'])
 run = FlipRun(fg, inits, cfg, bases=bases)
 for it in range(IT):

@@ -6,7 +6,7 @@ import numpy as np
 f, C = sys.argv[1], int(sys.argv[2])
 G = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 raw = np.fromfile(f, dtype=np.int64)
-S = 24 if (raw.size // C) % 24 == 0 else (16 if (raw.size // C) % 16 == 0 else 8)
+S = next(k for k in (28, 24, 16, 8) if (raw.size // C) % k == 0)
 rec = raw.reshape(-1, C, S)
 last = rec[-1].astype(np.float64)
 names = ["total", "draws", "eval", "commit", "book", "batches", "commit_it", "applied"]
@@ -36,6 +36,12 @@ if S >= 24:
         x = last[np.arange(C) % G == g].mean(axis=0)
         b = max(x[5], 1)
         print(f"{g:3d} | {x[16]/max(x[17],1):8.0f} {x[17]/b:6.2f} | {x[18]/max(x[12],1):8.0f} {x[19]/max(x[12],1):8.0f} {x[21]/max(x[12],1):6.2f}")
+if S >= 28:
+    print("grp | per batch: slots (proposal candidates), band rebuilds, cycles per rebuild")
+    for g in range(G):
+        x = last[np.arange(C) % G == g].mean(axis=0)
+        b = max(x[5], 1)
+        print(f"{g:3d} | {x[24]/b:6.2f} {x[22]/b:6.3f} {x[23]/max(x[22],1):8.0f}")
 print("max chain total Mcyc", last[:, 0].max() / 1e6, "argmax", int(last[:, 0].argmax()))
 tot = last[:, 0]
 print("per group total Mcyc mean / p90 / max:",
