@@ -369,9 +369,11 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     // allocated; FC_FLAG_FORCE_BFS keeps the search (cross-check)
     r->dgraph = !recom && k > 2 && k <= fc::kMaxKDistrictRule && g.n_exact == n && g.planar && g.outer_simple &&
                 !(p->flags & FC_FLAG_FORCE_BFS);
-    if (!recom && k > 2)  // fc_kernels.hip: a, fcnt, thresholds, [BFS scratch | district tables], slots,
-                          // district populations, wait queue
-        r->chain_lds_bytes = 2 * r->npad + (2 * R + 2) * 8 + (r->dgraph ? fc::dgraph_lds_bytes(k) : fc::bfs_bytes(n)) +
+    if (!recom && k > 2)  // fc_kernels.hip: a, fcnt (one packed byte per node with the district-graph
+                          // rule), thresholds, [BFS scratch | district tables], slots, district
+                          // populations, wait queue
+        r->chain_lds_bytes = (r->dgraph ? 1 : 2) * r->npad + (2 * R + 2) * 8 +
+                             (r->dgraph ? fc::dgraph_lds_bytes(k) : fc::bfs_bytes(n)) +
                              5 * 64 * 4 + fc::kMaxKGeneral * 4 + fc::kNfh * 4 + fc::kWaitQK * 16;
     // PAIR slot bound: fc_params.wmax > 0 fixes it; otherwise the canonical stream's bound is
     // the state's largest foreign-district count (kept on the device, r->wmax = 0)

@@ -60,9 +60,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     const int n = p.n;
     const int npad = (n + 15) & ~15;
     unsigned char *base = smem + (coop ? (size_t)0 : (size_t)wv * p.chain_lds_bytes);
+    // KM = 3 packs a node into one byte: district (bits 0-4) | foreign districts nf, saturated
+    // at 7 (bits 5-7); the exact nf is recounted from the ring where it matters (the slot
+    // filter of a saturated node, the nf histogram).  Half the chain's LDS: C4 / C5 hold about
+    // twice the chains per CU.  The HBM state keeps the exact int8 / uint8 arrays.
+    constexpr bool PK = KM == 3;
     int8_t *a = (int8_t *)base;
-    uint8_t *fcnt = base + npad;
-    uint64_t *T = (uint64_t *)(base + 2 * npad);
+    uint8_t *const pkb = base;                      // PK: the packed bytes (a aliases them)
+    uint8_t *fcnt = base + npad;                    // !PK
+    uint64_t *T = (uint64_t *)(base + (PK ? 1 : 2) * npad);
+    auto dist = [&](int u) -> int { return PK ? (int)(pkb[u] & 31u) : (int)a[u]; };
     BfsScratch bs;                                  // BFS labels, masks, chunk, bitmaps
     bs.lab = (uint32_t *)(T + (2 * RMAX + 2));
     bs.lab_words = p.lab_words;
@@ -106,8 +113,25 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         const uint4 *ga = (const uint4 *)(p.assign + (size_t)c * npad);
         const uint4 *gf = (const uint4 *)(p.fcnt + (size_t)c * npad);
         for (int i = lane; i < npad / 16; i += kWave) {
-            ((uint4 *)a)[i] = ga[i];
-            ((uint4 *)fcnt)[i] = gf[i];
+            if constexpr (PK) {
+                const uint4 x = ga[i], y = gf[i];
+                const uint32_t xa[4] = {x.x, x.y, x.z, x.w}, ya[4] = {y.x, y.y, y.z, y.w};
+                uint32_t o[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const uint32_t f = (ya[q] >> (8 * b)) & 0xffu;
+                        w |= (((xa[q] >> (8 * b)) & 31u) | ((f < 7u ? f : 7u) << 5)) << (8 * b);
+                    }
+                    o[q] = w;
+                }
+                ((uint4 *)pkb)[i] = uint4{o[0], o[1], o[2], o[3]};
+            } else {
+                ((uint4 *)a)[i] = ga[i];
+                ((uint4 *)fcnt)[i] = gf[i];
+            }
         }
         if (lane < 2 * RMAX + 1) T[lane] = p.thresh[(size_t)c * (2 * RMAX + 1) + lane];
         if (KM != 2 && lane < 32) {
@@ -225,7 +249,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 // (a slot rejected by the Lemire map never proposes: not a non-hit either)
                 const uint64_t mw = (uint64_t)w.x3 * (uint64_t)(uint32_t)wcap;
                 ok = ok && (uint32_t)mw >= wthr;
-                hit = ok && (int)(mw >> 32) < (int)fcnt[v];
+                if constexpr (PK) {  // a saturated count passes every slot; 1b decides exactly
+                    const int nfs = (int)(pkb[v] >> 5);
+                    hit = ok && ((int)(mw >> 32) < nfs || nfs == 7);
+                } else {
+                    hit = ok && (int)(mw >> 32) < (int)fcnt[v];
+                }
             } else {
                 hit = ok && fcnt[v] != 0;
             }
@@ -265,7 +294,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         const int v = has ? (int)slot[lane] : 0;
         const uint32_t w1 = slot[64 + lane], w2 = slot[128 + lane];
         const NodeRec<RMAX> rec = G[v];
-        const int av = a[v];
+        const int av = dist(v);
         const int pv = rec.pop;
         const uint32_t Ln = (uint32_t)(rec.meta & kMetaLenMask);
         const uint32_t full = (1u << Ln) - 1u;
@@ -277,6 +306,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         bool slot_ok = true;
         int adv[RMAX];       // districts of the ring cells (KM = 0)
         int nf_after = 0;    // KM != 2: foreign districts of v after its flip
+        int nf_before = 0;   // ... and before it
         if constexpr (KM == 2) {
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) inA |= (uint32_t)(a[ring_entry<RMAX>(rec.ring, i)] == av) << i;
@@ -287,7 +317,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             uint32_t dall = 0;                  // districts among the neighbours
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) {
-                adv[i] = a[ring_entry<RMAX>(rec.ring, i)];
+                adv[i] = dist(ring_entry<RMAX>(rec.ring, i));
                 inA |= (uint32_t)(adv[i] == av) << i;
                 if ((nbr >> i) & 1u) dall |= 1u << adv[i];
             }
@@ -302,6 +332,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             for (int q = 0; q < r && dd; ++q) dd &= dd - 1u;
             tgt = dd ? __builtin_ctz(dd) : 0;
             nf_after = __popc(dall & ~(1u << tgt));
+            nf_before = __popc(dm);
             tmask = 0;
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) tmask |= (uint32_t)(adv[i] == tgt) << i;
@@ -360,7 +391,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                     while (run) {
                         const int i = __builtin_ctz(run);
                         run &= run - 1u;
-                        dR |= 1u << (int)a[ring_entry<RMAX>(rec.ring, i)];
+                        dR |= 1u << dist(ring_entry<RMAX>(rec.ring, i));
                     }
                     s_cut = (dR & seen) != 0;
                     seen |= dR;
@@ -372,8 +403,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         // packed for the wave-uniform apply
         const uint32_t pk = (uint32_t)v | ((uint32_t)av << 15) | ((uint32_t)tgt << 21) | ((uint32_t)gam << 27);
         const uint32_t pk2 = inA | (nbr << 16);
-        // |delta| <= deg <= 16; nf_after <= 16
-        const uint32_t pk3 = tmask | ((uint32_t)(delta + 32) << 16) | ((uint32_t)nf_after << 24);
+        // |delta| <= deg <= 16 (6 bits); nf_after, nf_before <= 16 (5 bits each)
+        const uint32_t pk3 = tmask | ((uint32_t)(delta + 32) << 16) | ((uint32_t)nf_after << 22) |
+                             ((uint32_t)nf_before << 27);
         FC_STAMP(t_c);
         FC_PROF(2, t_c - t_b);
 
@@ -385,7 +417,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         const int cut0 = cut, nb0 = nb, rem0 = rem;
         const int64_t steps0 = steps;
         const int last_flip0 = last_flip;
-        const int a_last0 = last_flip0 >= 0 ? (int)a[last_flip0] : 0;
+        const int a_last0 = last_flip0 >= 0 ? dist(last_flip0) : 0;
         int cut_after = 0, nb_after = 0;
         // contiguity undecided by the ring rule at slot f: wave BFS on the current state
         auto run_bfs = [&](int f) -> bool {
@@ -488,7 +520,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             const uint32_t pkf = rlu(pk, f), pk2f = rlu(pk2, f), pk3f = rlu(pk3, f);
             const int vf = (int)(pkf & 0x7fffu), Af = (int)((pkf >> 15) & 63u), tf = (int)((pkf >> 21) & 63u);
             const bool gamf = (pkf >> 27) & 1u;
-            const int df = (int)((pk3f >> 16) & 0xffu) - 32;
+            const int df = (int)((pk3f >> 16) & 0x3fu) - 32;
             const int pvf = rl32(pv, f);
             const uint32_t inAf = pk2f & 0xffffu, nbrf = pk2f >> 16, tmf = pk3f & 0xffffu;
             uint32_t rw[RMAX / 2];
@@ -516,20 +548,31 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 // foreign districts nf(u) of vf's neighbours, recounted on the new state (v
                 // leaving A can drop A from u's foreign set, joining T add T), and vf's own
                 // from the evaluation; nfh follows every change, and with it the slot bound
-                if (lane == 0) a[vf] = (int8_t)tf;
+                const int nf_af = (int)((pk3f >> 22) & 31u), nf_bf = (int)(pk3f >> 27);
+                if (lane == 0) {
+                    if constexpr (PK) pkb[vf] = (uint8_t)(tf | ((nf_af < 7 ? nf_af : 7) << 5));
+                    else a[vf] = (int8_t)tf;
+                }
                 compiler_fence();
                 if (is_nbr) {
                     const NodeRec<RMAX> ru = G[my_e];
-                    const int au = a[my_e];
+                    const int au = dist(my_e);
                     const uint32_t nbu = (uint32_t)(ru.meta >> kMetaNbrShift) & 0xffffu;
-                    uint32_t du = 0;
+                    uint32_t du = 0, du0 = 0;  // districts among u's neighbours after / before the flip
 #pragma unroll
                     for (int i = 0; i < RMAX; ++i)
-                        if ((nbu >> i) & 1u) du |= 1u << a[ring_entry<RMAX>(ru.ring, i)];
+                        if ((nbu >> i) & 1u) {
+                            const int w = ring_entry<RMAX>(ru.ring, i);
+                            const int xw = dist(w);
+                            du |= 1u << xw;
+                            du0 |= 1u << (w == vf ? Af : xw);
+                        }
                     const int nfn = __popc(du & ~(1u << au));
-                    const int old = fcnt[my_e];
+                    // the old count: exact from the ring when packed (a stored 7 may stand for more)
+                    const int old = PK ? __popc(du0 & ~(1u << au)) : (int)fcnt[my_e];
                     if (nfn != old) {
-                        fcnt[my_e] = (uint8_t)nfn;
+                        if constexpr (PK) pkb[my_e] = (uint8_t)(au | ((nfn < 7 ? nfn : 7) << 5));
+                        else fcnt[my_e] = (uint8_t)nfn;
                         atomicSub(&nfh[old], 1);
                         atomicAdd(&nfh[nfn], 1);
                     }
@@ -538,11 +581,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                     grew = nfn > old;
                 }
                 if (lane == 0) {
-                    const int old = fcnt[vf], nfn = (int)((pk3f >> 24) & 31u);
-                    if (nfn != old) {
-                        fcnt[vf] = (uint8_t)nfn;
+                    // vf's own count: before / after from its evaluation (its view was current)
+                    const int old = PK ? nf_bf : (int)fcnt[vf];
+                    if (nf_af != old) {
+                        if constexpr (!PK) fcnt[vf] = (uint8_t)nf_af;
                         atomicSub(&nfh[old], 1);
-                        atomicAdd(&nfh[nfn], 1);
+                        atomicAdd(&nfh[nf_af], 1);
                     }
                 }
                 if (p.wdyn) {
@@ -572,7 +616,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 const int Lf = rl32((int)Ln, f);
                 bool chg = false;
                 if (lane < Lf) {
-                    const int X = a[my_e];
+                    const int X = dist(my_e);
                     if (X != Af && atomicSub(&mcnt[min(Af, X) * p.k + max(Af, X)], 1) == 1) {
                         atomicAnd(&adj[Af], ~(1u << X));
                         atomicAnd(&adj[X], ~(1u << Af));
@@ -858,8 +902,36 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
         uint4 *ga = (uint4 *)(p.assign + (size_t)c * npad);
         uint4 *gf = (uint4 *)(p.fcnt + (size_t)c * npad);
         for (int i = lane; i < npad / 16; i += kWave) {
-            ga[i] = ((const uint4 *)a)[i];
-            gf[i] = ((const uint4 *)fcnt)[i];
+            if constexpr (PK) {
+                const uint4 x = ((const uint4 *)pkb)[i];
+                const uint32_t xa[4] = {x.x, x.y, x.z, x.w};
+                uint32_t oa[4], of[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    oa[q] = xa[q] & 0x1f1f1f1fu;
+                    of[q] = (xa[q] >> 5) & 0x07070707u;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        if (((of[q] >> (8 * b)) & 0xffu) != 7u) continue;
+                        // saturated: the exact count from the ring (rare)
+                        const int u = 16 * i + 4 * q + b;
+                        const NodeRec<RMAX> ru = G[u];
+                        const int au = (int)(pkb[u] & 31u);
+                        const uint32_t nbu = (uint32_t)(ru.meta >> kMetaNbrShift) & 0xffffu;
+                        uint32_t du = 0;
+                        for (int j = 0; j < RMAX; ++j)
+                            if ((nbu >> j) & 1u) du |= 1u << dist(ring_entry<RMAX>(ru.ring, j));
+                        of[q] = (of[q] & ~(0xffu << (8 * b))) | ((uint32_t)__popc(du & ~(1u << au)) << (8 * b));
+                    }
+                ga[i] = uint4{oa[0], oa[1], oa[2], oa[3]};
+                gf[i] = uint4{of[0], of[1], of[2], of[3]};
+            } else {
+                ga[i] = ((const uint4 *)a)[i];
+                gf[i] = ((const uint4 *)fcnt)[i];
+            }
         }
         if (KM != 2 && lane < 32) {
             p.popk[(size_t)c * 32 + lane] = popk[lane];

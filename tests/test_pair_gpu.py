@@ -261,8 +261,8 @@ def test_instance_selection_and_agreement(gpu, sec11):
     r2 = [_run_pair(sec11, i2, b2, 2, steps=steps, pct=0.1, flags=f, proposal=_lib.FC_PROPOSE_BI_SIGN)
           for f in (0, _lib.FC_FLAG_FORCE_BFS)]
     # (every chain traced: the XTRA diagnostics instance, SEARCH the fourth parameter)
-    assert r2[0].kernel_name().endswith(", true, false, true>"), r2[0].kernel_name()
-    assert r2[1].kernel_name().endswith(", true, true, true>"), r2[1].kernel_name()
+    assert r2[0].kernel_name().endswith(", true, false, true, false>"), r2[0].kernel_name()
+    assert r2[1].kernel_name().endswith(", true, true, true, false>"), r2[1].kernel_name()
     for key in ("steps", "proposals", "accepted", "sum_cut", "sum_nb", "sum_wait", "cut", "nb"):
         assert np.array_equal(r2[0].stats()[key], r2[1].stats()[key]), key
     assert np.array_equal(r2[0].state(), r2[1].state())
@@ -300,3 +300,28 @@ def test_pair_slot_bound_long_chain_across_launches(gpu, cref, chunks):
     bases = np.asarray([1.0, 0.5, 1.0, 3.0, 1.0, 0.25])
     run = _run_pair(spec, inits, bases, k, steps=9000, pct=0.3, chunks=chunks)
     _check(cref, spec, run, k, inits, bases, steps=9000, pct=0.3)
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_packed_node_bytes_saturated_counts(gpu, cref, chunks):
+    """The district-rule instance packs a node into one byte (district | foreign districts
+    saturated at 7).  A wheel whose hub, alone in district 0, touches eight rim districts has a
+    saturated count from the start: the slot filter passes it to the exact recount, the nf
+    histogram (the canonical slot bound) follows exact counts, and the write-back restores the
+    exact count between launches.  Per proposal against the oracle, in one and three launches."""
+    import math
+    import networkx as nx
+    m, k = 15, 9
+    g = nx.wheel_graph(m + 1)  # hub 0, rim 1..m
+    pos = {0: (0.0, 0.0)}
+    pos.update({i: (math.cos(2 * math.pi * i / m), math.sin(2 * math.pi * i / m)) for i in range(1, m + 1)})
+    spec = G.from_networkx(g, pos=pos)
+    a0 = np.zeros(spec.n, dtype=np.int8)
+    for i in range(1, m + 1):  # districts 1..7 two rim nodes each, district 8 the last one
+        a0[spec.index[i]] = min((i - 1) // 2 + 1, k - 1)
+    inits = np.stack([a0] * 12)
+    bases = np.asarray([[0.5, 1.0, 3.0][c % 3] for c in range(12)])
+    run = _run_pair(spec, inits, bases, k, steps=3000, pct=0.9, chunks=chunks)
+    assert run.kernel_name().startswith("fc::flip_kernel<16, "), run.kernel_name()
+    assert ", 3, " in run.kernel_name()  # the district-rule (packed) instance
+    _check(cref, spec, run, k, inits, bases, steps=3000, pct=0.9)

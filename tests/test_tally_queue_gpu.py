@@ -35,7 +35,7 @@ def test_k2_tally_queue(gpu, cref, sec11, wait_queue, waits):
     run = FlipRun(FlipGraph(sec11), inits, cfg, bases=bases)
     for n in LAUNCHES:
         run.steps(n)
-    assert run.kernel_name().startswith("fc::flip2_kernel<8, 4, true, false, false>"), run.kernel_name()
+    assert run.kernel_name().startswith("fc::flip2_kernel<8, 4, true, false, false, false>"), run.kernel_name()
     st = run.stats()
     ch, nh = run.hist()
     ct = run.cut_times()
