@@ -6,7 +6,8 @@ import numpy as np
 
 raw = np.fromfile(sys.argv[1], dtype=np.int64)
 C, G = int(sys.argv[2]), int(sys.argv[3]) if len(sys.argv) > 3 else 1
-last = raw.reshape(-1, C, 24)[-1].astype(np.float64)
+S = next(k for k in (28, 24) if (raw.size // C) % k == 0)  # fc_internal.h kProfSlots
+last = raw.reshape(-1, C, S)[-1].astype(np.float64)
 for g in range(G):
     x = last[np.arange(C) % G == g].mean(axis=0)
     b, fl = max(x[5], 1), max(x[7], 1)
