@@ -17,7 +17,9 @@ CSRC = os.path.join(PKG, "csrc")
 # (prof: per-phase s_memtime counters; sync: each stamp drains outstanding memory first).
 VARIANT = os.environ.get("FC_LIB_VARIANT", "")
 VARIANT_FLAGS = {"prof": "-DFC_PHASE_PROF", "sync": "-DFC_PHASE_SYNC", "mask": "-DFC_MASKED_STORES",
-                 "dupnf": "-DFC_EXP_DUP_NF", "dupdg": "-DFC_EXP_DUP_DG"}
+                 "dupnf": "-DFC_EXP_DUP_NF", "dupdg": "-DFC_EXP_DUP_DG",
+                 "dupdraw": "-DFC_EXP_DUP_DRAW", "dupeval": "-DFC_EXP_DUP_EVAL", "dupmarks": "-DFC_EXP_DUP_MARKS",
+                 "dupapply": "-DFC_EXP_DUP_APPLY"}
 LIB = os.environ.get("FC_LIB_OUT") or os.path.join(PKG, f"libflipchain_{VARIANT}.so" if VARIANT else "libflipchain.so")
 SOURCES = ["fc_flip2.hip", "fc_deal.hip", "fc_kernels.hip", "fc_series.hip", "fc_recom.hip", "fc_capi.cpp", "fc_graph.cpp"]
 HEADERS = ["fc_internal.h", "fc_philox.h", "fc_device.h", "fc_ring.h", os.path.join("..", "..", "include", "flipchain.h")]

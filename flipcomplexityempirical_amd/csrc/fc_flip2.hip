@@ -352,6 +352,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 }
 #else
                 w = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
+#ifdef FC_EXP_DUP_DRAW
+                {  // timing experiment only: a second Philox per draw, discarded
+                    const Words4 wx = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 7u, p.seed_lo, p.seed_hi);
+                    asm volatile("" ::"v"(wx.x0 ^ wx.x1 ^ wx.x2 ^ wx.x3));
+                }
+#endif
 #endif
             }
             int vd;
@@ -409,6 +415,15 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         int v = has ? (int)slot[lane] : 0;
         const uint32_t w1 = slot[64 + lane], w2 = slot[128 + lane];
         const NodeRec<RMAX> rec = G[v];
+#ifdef FC_EXP_DUP_EVAL
+        {  // timing experiment only: the slot's record and ring districts once more, discarded
+            const NodeRec<RMAX> rx = G[v ^ 0];
+            uint32_t ix = 0;
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) ix |= (uint32_t)a[ring_entry<RMAX>(rx.ring, i)] << i;
+            asm volatile("" ::"v"(ix));
+        }
+#endif
         int av = a[v];
         int pv = rec.pop;
         const uint32_t Ln = (uint32_t)(rec.meta & kMetaLenMask);
@@ -684,6 +699,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         need = need && again;
                         if (!__any(need)) break;
                     }
+#ifdef FC_EXP_DUP_MARKS
+                    {  // timing experiment only: the marks' reads once more, discarded
+                        int xs = smark[v];
+#pragma unroll
+                        for (int i = 0; i < RMAX; ++i) xs += nmark[cell[i]] + smark[cell[i]];
+                        asm volatile("" ::"v"(xs));
+                    }
+#endif
                     FC_STAMP(t_mk);
                     FC_PROF(18, t_mk - t_it1);
                     bool conf = ms < lane;
@@ -863,6 +886,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             bool enter = false, leave = false, outS = false;
             if (is_nbr) {
                 const int old = fcnt[my_e];
+#ifdef FC_EXP_DUP_APPLY
+                {  // timing experiment only: the neighbour's count read once more, discarded
+                    const int ox = fcnt[my_e ^ 0];
+                    asm volatile("" ::"v"(ox));
+                }
+#endif
                 const uint64_t swd = BAND ? sb[my_e >> 6] : 0ull;
                 fcnt[my_e] = (uint8_t)(old + dlt);
                 enter = dlt > 0 && old == 0;
