@@ -13,7 +13,7 @@ from . import build as _build
 _P = ctypes.POINTER
 
 STREAM_NODE, STREAM_BAND = 0, 1  # include/flipchain.h FC_STREAM_*
-FC_ABI_VERSION = 4  # include/flipchain.h: fc_params layout version
+FC_ABI_VERSION = 5  # include/flipchain.h: fc_params layout version
 
 FC_OK = 0
 FC_ERR_ARG = -1
@@ -70,7 +70,7 @@ class Params(ctypes.Structure):
                 # per-chain configuration
                 ("chain_pop_bounds", _P(ctypes.c_int64)),
                 # k = 2 node stream: FC_STREAM_NODE / FC_STREAM_BAND
-                ("stream", ctypes.c_int32)]
+                ("stream", ctypes.c_int32), ("tune_multi_flip", ctypes.c_int32)]
 
 
 class ChainStats(ctypes.Structure):

@@ -155,6 +155,7 @@ struct KParams {
     uint32_t *ctime;            // [n_chains] draws each chain took in its last launch (the dealing key)
     // k = 2 band stream (FC_STREAM_BAND): per chain the band S = b_nodes + neighbours as a
     // bitmap of `words` u64; a draw selects the i-th member (fc_flip2.hip)
+    int32_t multi_flip;         // k > 2 district-rule instance: several independent flips per commit pass
     int32_t band;
     int32_t band_step0;         // largest power of two below `words` (rank search over the words)
     uint64_t *sbits;            // [n_chains * words]

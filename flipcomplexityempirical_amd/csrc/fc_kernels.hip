@@ -47,7 +47,9 @@ using namespace dev;
 // RMAX = 8: at most 128 VGPRs, four waves per SIMD (C3's 8192 chains per GPU run in two
 // rounds of waves instead of three: 1.46e9 against 1.35e9 proposals/s; a handful of VGPRs
 // spill, which costs C4's LDS-limited launch 2 %)
-template <int RMAX, int NSUB, int KM, bool FULL>
+// MF (KM = 3, RMAX = 8 only): the multi-flip commit below, in an instance of its own so that
+// runs without it keep the smaller code
+template <int RMAX, int NSUB, int KM, bool FULL, bool MF>
 __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
@@ -100,6 +102,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     uint32_t *adj = (uint32_t *)(mcnt + p.k * p.k);
     int32_t *ngk = (int32_t *)(adj + 32);
     const bool dgraph = KM == 3 || (KM != 2 && p.dgraph != 0);  // KM = 3: always, by construction
+    // KM = 3 multi-flip commit: marks of the members' neighbours, hashed to 2048 bits (a
+    // collision only ends a group early)
+    uint32_t *hb = (uint32_t *)(ngk + 32);
     // cooperative search control words (coop implies no district tables: they start here)
     int32_t *ctl = (int32_t *)(q_run + kWaitQK);
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
@@ -142,6 +147,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             const int kk = p.k * p.k;
             for (int i = lane; i < kk; i += kWave) mcnt[i] = p.mcnt[(size_t)c * kk + i];
             if (lane < 32) ngk[lane] = p.ngk[(size_t)c * 32 + lane];
+            if (KM == 3 && MF) hb[lane] = 0u;
             wave_sync();
             // adj[X] bit Y: some face holds cells of X and Y; bit 31: X touches the outer face
             uint32_t m = 0;
@@ -514,6 +520,225 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 const bool res = run_bfs(f);
                 if (lane == f) st |= ST_BD | (res ? ST_BR : 0u);
                 continue;
+            }
+
+            // ---- KM = 3: several independent flips in one pass -----------------------------
+            // The accepted slots after f are taken in slot order while they stay independent of
+            // the ones taken before them: no taken node in a later slot's ring or as its node
+            // (that slot's view would change: the batch ends there), no shared neighbour (the
+            // neighbours' foreign-district recounts would need an order), no later proposal whose
+            // population verdict changes under the taken flips.  Their neighbours' recounts run in
+            // parallel (lane group g = the g-th flip), then the district tables and the nf histogram
+            // take the flips one by one in slot order, and the first flip that changes an adjacency
+            // bit or the slot bound is the last one applied -- exactly the one-flip-at-a-time chain.
+            if constexpr (KM == 3 && MF) {
+                constexpr int kGrp = 64 / RMAX;  // flips per pass (one lane per ring cell)
+                const uint64_t CANDM = __ballot(valid && acc) & lane_range(f, end);
+                if (__popcll(CANDM) >= 2) {
+                    FC_PROF(21, 1);
+                    uint64_t FM = 0;
+                    int nF = 0;
+                    int cutA = end;     // first slot whose view a taken flip changed (the batch ends there)
+                    int cutP = kWave;   // first proposal whose population verdict changed
+                    int dA = 0, dT = 0; // this slot's district populations moved by the taken flips
+                    const int gi = lane / RMAX, ge = lane % RMAX;
+                    for (uint64_t CC = CANDM; CC && nF < kGrp; CC &= CC - 1ull) {
+                        const int i = __builtin_ctzll(CC);
+                        if (i >= cutA || i >= cutP) break;
+                        const int vi = rl32(v, i);
+                        const uint32_t pki = rlu(pk, i), nbri = rlu(pk2, i) >> 16;
+                        const int Ai = (int)((pki >> 15) & 63u), Ti = (int)((pki >> 21) & 63u);
+                        const int pvi = rl32(pv, i);
+                        uint32_t rwi[RMAX / 2];
+#pragma unroll
+                        for (int k2 = 0; k2 < RMAX / 2; ++k2) rwi[k2] = rlu(rec.ring[k2], i);
+                        // its neighbours against the marks of the flips taken before it
+                        uint32_t sel = rwi[0];
+#pragma unroll
+                        for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((ge >> 1) == k2) ? rwi[k2] : sel;
+                        const int ui = (int)((sel >> (16 * (ge & 1))) & 0xffffu);
+                        const bool isn = gi == 0 && ((nbri >> ge) & 1u);
+                        if (nF > 0) {
+                            const bool clash = isn && ((hb[(ui & 2047) >> 5] >> (ui & 31)) & 1u);
+                            if (__any(clash)) break;
+                        }
+                        if (isn) atomicOr(&hb[(ui & 2047) >> 5], 1u << (ui & 31));
+                        FM |= 1ull << i;
+                        ++nF;
+                        // later slots whose node is vi or in its ring (rings are symmetric)
+                        bool stl = v == vi;
+#pragma unroll
+                        for (int k = 0; k < RMAX; ++k) stl |= v == (int)((rwi[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+                        const uint64_t SM = __ballot(stl && has && lane > i && lane < end);
+                        if (SM && __builtin_ctzll(SM) < cutA) cutA = __builtin_ctzll(SM);
+                        // the populations of later slots' districts after this flip
+                        dA += (av == Ti ? pvi : 0) - (av == Ai ? pvi : 0);
+                        dT += (tgt == Ti ? pvi : 0) - (tgt == Ai ? pvi : 0);
+                        const bool pok2 = (pa + dA - pv >= pop_lo) && (pb + dT + pv <= pop_hi);
+                        const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
+                        if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
+                    }
+                    const int f_last = 63 - __builtin_clzll(FM);
+                    const int nv = __popcll(VAL & lane_range(f, f_last + 1));
+                    // the flip taken g-th, its data, and this lane's ring cell of it
+                    const int mg = gi < nF ? select_bit64(FM, gi) : f;
+                    const uint32_t pkm = (uint32_t)__shfl((int)pk, mg), pk2m = (uint32_t)__shfl((int)pk2, mg),
+                                   pk3m = (uint32_t)__shfl((int)pk3, mg);
+                    const int vm = (int)(pkm & 0x7fffu), Am = (int)((pkm >> 15) & 63u), Tm = (int)((pkm >> 21) & 63u);
+                    const uint32_t nbrm = pk2m >> 16;
+                    uint32_t selm = 0;
+#pragma unroll
+                    for (int k2 = 0; k2 < RMAX / 2; ++k2) {
+                        const uint32_t w = (uint32_t)__shfl((int)rec.ring[k2], mg);
+                        if ((ge >> 1) == k2) selm = w;
+                    }
+                    const int um = (int)((selm >> (16 * (ge & 1))) & 0xffffu);
+                    const bool in_g = gi < nF;
+                    const bool nb_m = in_g && ((nbrm >> ge) & 1u);
+                    // exact recount of the neighbour's foreign districts before / after its flip,
+                    // reading the flipped node's district as Am / Tm (nothing is written yet)
+                    int old_m = 0, nfn_m = 0, au_m = 0;
+                    if (nb_m) {
+                        const NodeRec<RMAX> ru = G[um];
+                        au_m = dist(um);
+                        const uint32_t nbu = (uint32_t)(ru.meta >> kMetaNbrShift) & 0xffffu;
+                        uint32_t du = 0, du0 = 0;
+#pragma unroll
+                        for (int k = 0; k < RMAX; ++k)
+                            if ((nbu >> k) & 1u) {
+                                const int w = ring_entry<RMAX>(ru.ring, k);
+                                const int xw = w == vm ? Tm : dist(w);
+                                du |= 1u << xw;
+                                du0 |= 1u << (w == vm ? Am : xw);
+                            }
+                        nfn_m = __popc(du & ~(1u << au_m));
+                        old_m = __popc(du0 & ~(1u << au_m));
+                    }
+                    const bool grew_m = nb_m && nfn_m > old_m;
+                    // entering non-hit draws: the flip's grown node drawn later as a non-hit
+                    int t_na = trunc_off;
+                    {
+                        const int off_m = __shfl(off_l, mg);
+                        uint64_t ge_m = __ballot(grew_m);
+                        while (ge_m) {
+                            const int ln = __builtin_ctzll(ge_m);
+                            ge_m &= ge_m - 1ull;
+                            const int u = rl32(um, ln), ofm = rl32(off_m, ln);
+#pragma unroll
+                            for (int r = 0; r < NSUB; ++r) {
+                                const uint64_t m2 = __ballot(((nonhit[r] >> lane) & 1ull) && rv[r] == u && 64 * r + lane > ofm);
+                                if (m2 && 64 * r + __builtin_ctzll(m2) < t_na) t_na = 64 * r + __builtin_ctzll(m2);
+                            }
+                        }
+                    }
+                    const int e2 = t_na < trunc_off ? __popcll(__ballot(has && off_l < t_na)) : kWave;
+                    if (nF < 2 || nv >= rem || e2 <= f_last) {
+                        // not worth it, or the launch's last step / an entering draw lies inside:
+                        // clear the marks and take f alone
+                        if (nb_m) hb[(um & 2047) >> 5] = 0u;
+                        compiler_fence();
+                    } else {
+                        // district tables and nf histogram flip by flip, in slot order
+                        int nA_ = 0;  // flips applied
+                        bool adj_chg = false, wcap_chg = false;
+                        const int Lm = __shfl((int)Ln, mg);
+                        const bool gamm = (pkm >> 27) & 1u;
+                        const int nf_af = (int)((pk3m >> 22) & 31u), nf_bf = (int)(pk3m >> 27);
+                        for (int g = 0; g < nF; ++g) {
+                            bool chg = false;
+                            if (gi == g && ge < Lm) {
+                                const int X = dist(um);
+                                if (X != Am && atomicSub(&mcnt[min(Am, X) * p.k + max(Am, X)], 1) == 1) {
+                                    atomicAnd(&adj[Am], ~(1u << X));
+                                    atomicAnd(&adj[X], ~(1u << Am));
+                                    chg = true;
+                                }
+                                if (X != Tm && atomicAdd(&mcnt[min(Tm, X) * p.k + max(Tm, X)], 1) == 0) {
+                                    atomicOr(&adj[Tm], 1u << X);
+                                    atomicOr(&adj[X], 1u << Tm);
+                                    chg = true;
+                                }
+                            }
+                            if (gi == g && ge == 0 && gamm) {
+                                if (atomicSub(&ngk[Am], 1) == 1) {
+                                    atomicAnd(&adj[Am], ~(1u << 31));
+                                    atomicAnd(&adj[31], ~(1u << Am));
+                                    chg = true;
+                                }
+                                if (atomicAdd(&ngk[Tm], 1) == 0) {
+                                    atomicOr(&adj[Tm], 1u << 31);
+                                    atomicOr(&adj[31], 1u << Tm);
+                                    chg = true;
+                                }
+                            }
+                            if (gi == g && nb_m && nfn_m != old_m) {
+                                atomicSub(&nfh[old_m], 1);
+                                atomicAdd(&nfh[nfn_m], 1);
+                            }
+                            if (gi == g && ge == 0 && nf_af != nf_bf) {
+                                atomicSub(&nfh[nf_bf], 1);
+                                atomicAdd(&nfh[nf_af], 1);
+                            }
+                            ++nA_;
+                            adj_chg = __any(chg);
+                            if (p.wdyn) {
+                                compiler_fence();
+                                const uint64_t hm = __ballot(lane >= 1 && lane < kNfh && nfh[lane] > 0);
+                                const int wn = hm ? 63 - __builtin_clzll(hm) : 1;
+                                if (wn != wcap) {
+                                    wcap = wn;
+                                    wthr = (0u - (uint32_t)wcap) % (uint32_t)wcap;
+                                    wcap_chg = true;
+                                }
+                            }
+                            if (adj_chg || wcap_chg) break;
+                        }
+                        // the flips applied: districts and counts, populations, marks cleared
+                        const bool app = gi < nA_;
+                        const int pvm = __shfl(pv, mg);
+                        if (nb_m) hb[(um & 2047) >> 5] = 0u;
+                        if (app && ge == 0) {
+                            pkb[vm] = (uint8_t)(Tm | ((nf_af < 7 ? nf_af : 7) << 5));
+                            atomicSub(&popk[Am], pvm);
+                            atomicAdd(&popk[Tm], pvm);
+                        }
+                        if (app && nb_m && nfn_m != old_m) pkb[um] = (uint8_t)(au_m | ((nfn_m < 7 ? nfn_m : 7) << 5));
+                        const bool ent_m = app && nb_m && old_m == 0 && nfn_m > 0;
+                        const bool lev_m = app && nb_m && old_m > 0 && nfn_m == 0;
+                        // the slots up to the last flip applied: verdict bits, |cut| / |B| after each flip
+                        const int fl = select_bit64(FM, nA_ - 1);
+                        if (prop && lane >= f && lane <= fl) st |= bits;
+                        for (int g = 0; g < nA_; ++g) {
+                            const int lg = select_bit64(FM, g);
+                            cut += (int)((rlu(pk3, lg) >> 16) & 0x3fu) - 32;
+                            nb += __popcll(__ballot(ent_m && gi == g)) - __popcll(__ballot(lev_m && gi == g));
+                            if (lane == lg) {
+                                st |= ST_VS | ST_AC;
+                                cut_after = cut;
+                                nb_after = nb;
+                            }
+                        }
+                        rem -= __popcll(VAL & lane_range(f, fl + 1));
+                        last_flip = rl32(v, fl);
+                        compiler_fence();
+                        FC_PROF(7, nA_);
+                        FC_PROF(22, nA_);
+                        // what ends the batch after them: a changed view, adjacency or slot bound, an
+                        // entering draw
+                        if (cutA < end) end = cutA;
+                        if ((adj_chg || wcap_chg) && fl + 1 < end) end = fl + 1;
+                        if (wcap_chg) {
+                            const int t_w = rl32(off_l, fl) + 1;
+                            if (t_w < trunc_off) trunc_off = t_w;
+                        }
+                        if (t_na < trunc_off) {
+                            trunc_off = t_na;
+                            if (e2 < end) end = e2;
+                        }
+                        pos = fl + 1;
+                        continue;
+                    }
+                }
             }
             // ---- accept slot f: apply the flip -----------------------------------------
             FC_PROF(7, 1);
@@ -1017,13 +1242,21 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, siz
     // hitting-time window; the lean instance (proposals, steps, sums, waits) keeps its
     // register budget for the hot loop.
     const bool full = p.tape || p.trace || (p.diag & ~(uint32_t)FC_DIAG_WAIT) || p.hit_lo <= p.hit_hi;
-#define FC_LAUNCH(R, S, K, F)                                                                           \
+#define FC_LAUNCHM(R, S, K, F, M)                                                                       \
     do {                                                                                                \
         if (lds > 65536)                                                                                \
-            (void)hipFuncSetAttribute((const void *)flip_kernel<R, S, K, F>,                            \
+            (void)hipFuncSetAttribute((const void *)flip_kernel<R, S, K, F, M>,                         \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
-        if (name) snprintf(name, name_cap, "fc::flip_kernel<%d, %d, %d, %s>", R, S, K, F ? "true" : "false"); \
-        hipLaunchKernelGGL((flip_kernel<R, S, K, F>), grid, block, lds, s, p);                          \
+        if (name)                                                                                       \
+            snprintf(name, name_cap, "fc::flip_kernel<%d, %d, %d, %s%s>", R, S, K, F ? "true" : "false", \
+                     M ? ", true" : "");                                                                \
+        hipLaunchKernelGGL((flip_kernel<R, S, K, F, M>), grid, block, lds, s, p);                       \
+    } while (0)
+    // the multi-flip instance: district-graph rule, RMAX = 8, when the run asks for it
+#define FC_LAUNCH(R, S, K, F)                                                     \
+    do {                                                                          \
+        if (K == 3 && R == 8 && p.multi_flip) FC_LAUNCHM(R, S, K, F, (K == 3 && R == 8)); \
+        else FC_LAUNCHM(R, S, K, F, false);                                        \
     } while (0)
 #define FC_FULL_SWITCH(R, S, K)                          \
     do {                                                 \
@@ -1060,6 +1293,7 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, siz
 #undef FC_NSUB_SWITCH
 #undef FC_FULL_SWITCH
 #undef FC_LAUNCH
+#undef FC_LAUNCHM
     return (int)hipGetLastError();
 }
 

@@ -135,7 +135,7 @@ class RunConfig:
     recom_max_attempts: int = 0
     # launch tuning (fc_params.tune_*): scheduling only, never the trajectory; 0 = default.
     # Keys: nsub, hit_stop, par_min, wait_queue, chains_per_block, prio_div (3), prio_th (3),
-    # search_waves, deal.
+    # search_waves, deal, multi_flip.
     tune: Optional[Dict[str, object]] = None
     # k = 2 node stream (fc_params.stream): "node" draws over all n nodes, "band" over the band
     # S = b_nodes + neighbours; the chain's law is the same, the trajectory not
@@ -143,7 +143,7 @@ class RunConfig:
 
 
 TUNE_KEYS = ("nsub", "hit_stop", "par_min", "wait_queue", "chains_per_block", "prio_div", "prio_th",
-             "search_waves", "deal")
+             "search_waves", "deal", "multi_flip")
 
 
 def parse_tune(text: str) -> Dict[str, object]:

@@ -39,7 +39,7 @@ extern "C" {
 
 /* fc_params.struct_size / abi_version: a caller built against another layout of fc_params is
  * rejected (FC_ERR_ARG) instead of read past.  Bumped whenever fc_params changes.           */
-#define FC_ABI_VERSION 4u
+#define FC_ABI_VERSION 5u
 
 /* fc_graph_create flags */
 #define FC_GRAPH_NO_EXACT 0x1u   /* never trust the planar local contiguity rule            */
@@ -176,6 +176,10 @@ typedef struct fc_params {
      * S into b_nodes, S is rebuilt from that state.  Short boundaries then waste few draws.
      * k = 2, n <= 4096, no replay tape; oracle: fr_params.stream                               */
     int32_t stream;
+    int32_t tune_multi_flip;    /* k > 2 with the district-graph rule, rings of <= 8 cells: commit
+                                   several independent accepted flips per pass (0: auto = on for
+                                   graphs of >= 4096 nodes; 1: on; -1: one at a time).
+                                   Scheduling only, like every tune_* field                    */
 } fc_params;
 
 #define FC_STREAM_NODE 0

@@ -325,3 +325,43 @@ def test_packed_node_bytes_saturated_counts(gpu, cref, chunks):
     assert run.kernel_name().startswith("fc::flip_kernel<16, "), run.kernel_name()
     assert ", 3, " in run.kernel_name()  # the district-rule (packed) instance
     _check(cref, spec, run, k, inits, bases, steps=3000, pct=0.9)
+
+
+@pytest.mark.parametrize("case", ["c3_tight", "c4", "c5"])
+def test_multi_flip_commit_equals_one_at_a_time(gpu, cref, sec11, case):
+    """The district-rule instance commits several independent accepted flips per pass
+    (fc_params.tune_multi_flip; auto = on for graphs of >= 4096 nodes, forced on here): traced
+    per proposal against the oracle, and its
+    lean instance state for state against one flip at a time.  c3_tight: sec11 k = 4 with a 1 %
+    population tolerance (population verdicts change under the flips taken before them); c4 /
+    c5: the triangular lattice and the Delaunay graph, always-accept base 1 among the bases."""
+    if case == "c3_tight":
+        spec, k, pct, steps = sec11, 4, 0.01, 2000
+        a0 = spec.assignment_array(G.quadrant_plan(spec.nodes), list(range(k)))
+    elif case == "c4":
+        spec, k, pct, steps = G.triangular_graph(40, 78), 8, 0.1, 2000
+        a0 = spec.assignment_array(G.strip_plan(spec, k), list(range(k)))
+    else:
+        spec, k, pct, steps = G.delaunay_graph(2000, seed=0), 18, 0.1, 2000
+        a0 = spec.assignment_array(G.bisection_plan(spec, k), list(range(k)))
+    inits = np.stack([a0] * 12)
+    bases = np.asarray([1.0, 0.5, 2.0, 1.0] * 3)
+    run = _run_pair(spec, inits, bases, k, steps=steps, pct=pct, chunks=2, tune={"multi_flip": 1})
+    name = run.kernel_name()
+    assert ", 3, " in name, name
+    # the multi-flip instance exists for rings of <= 8 cells (C5's Delaunay rings take 16)
+    assert name.endswith(", true, true>") == (case != "c5"), name  # FULL (traced), multi-flip
+    _check(cref, spec, run, k, inits, bases, steps=steps, pct=pct)
+    fg = FlipGraph(spec)
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
+    outs = []
+    for tune in ({"multi_flip": 1}, {"multi_flip": -1}):
+        cfg = RunConfig(k=k, labels=tuple(range(k)), proposal=_lib.FC_PROPOSE_PAIR, seed=21, pop_lo=lo, pop_hi=hi,
+                        tune=tune)
+        r = FlipRun(fg, inits, cfg, bases=bases)
+        r.steps(steps // 2)
+        r.steps(steps - steps // 2)
+        outs.append((r.stats(), r.state()))
+    for key in STAT_KEYS + ["wait_cur"]:
+        assert np.array_equal(outs[0][0][key], outs[1][0][key]), key
+    assert np.array_equal(outs[0][1], outs[1][1])

@@ -18,3 +18,6 @@ for g in range(G):
           f"  commit/flip {x[3] / fl:.0f}  neighbours recounted {x[19] / fl:.2f}")
     print(f"  batch ends: stale view {x[11] / b:.3f}  entering non-hit {x[12] / b:.3f}  adj change {x[15] / b:.3f}"
           f"  slot-bound change {x[16] / b:.3f}")
+    if S >= 28 and x[21] > 0:
+        print(f"  multi-flip passes {x[21] / b:.2f} per batch, flips per pass {x[22] / max(x[21], 1):.2f}"
+              f" ({x[22] / fl:.2f} of the flips)")
