@@ -536,6 +536,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                 const uint64_t CANDM = __ballot(valid && acc) & lane_range(f, end);
                 if (__popcll(CANDM) >= 2) {
                     FC_PROF(21, 1);
+                    FC_STAMP(t_m0);
                     uint64_t FM = 0;
                     int nF = 0;
                     int cutA = end;     // first slot whose view a taken flip changed (the batch ends there)
@@ -578,6 +579,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                         const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
                         if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
                     }
+                    FC_STAMP(t_m1);
+                    FC_PROF(23, t_m1 - t_m0);
                     const int f_last = 63 - __builtin_clzll(FM);
                     const int nv = __popcll(VAL & lane_range(f, f_last + 1));
                     // the flip taken g-th, its data, and this lane's ring cell of it
@@ -632,67 +635,106 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                         }
                     }
                     const int e2 = t_na < trunc_off ? __popcll(__ballot(has && off_l < t_na)) : kWave;
+                    FC_STAMP(t_m2);
+                    FC_PROF(24, t_m2 - t_m1);
                     if (nF < 2 || nv >= rem || e2 <= f_last) {
+                        FC_PROF(27, 1);
                         // not worth it, or the launch's last step / an entering draw lies inside:
                         // clear the marks and take f alone
                         if (nb_m) hb[(um & 2047) >> 5] = 0u;
                         compiler_fence();
                     } else {
-                        // district tables and nf histogram flip by flip, in slot order
-                        int nA_ = 0;  // flips applied
+                        // district tables and nf histogram: all flips at once, decrements before
+                        // increments.  A count that reaches 0 there (or an increment from 0, or a slot
+                        // bound move) is the only way some prefix of the flips, taken in slot order, can
+                        // change an adjacency bit or the bound; otherwise all apply unchanged.  When
+                        // one might, the counts are restored and the flips go one by one.
+                        int nA_ = nF;  // flips applied
                         bool adj_chg = false, wcap_chg = false;
                         const int Lm = __shfl((int)Ln, mg);
                         const bool gamm = (pkm >> 27) & 1u;
                         const int nf_af = (int)((pk3m >> 22) & 31u), nf_bf = (int)(pk3m >> 27);
-                        for (int g = 0; g < nF; ++g) {
-                            bool chg = false;
-                            if (gi == g && ge < Lm) {
-                                const int X = dist(um);
-                                if (X != Am && atomicSub(&mcnt[min(Am, X) * p.k + max(Am, X)], 1) == 1) {
-                                    atomicAnd(&adj[Am], ~(1u << X));
-                                    atomicAnd(&adj[X], ~(1u << Am));
-                                    chg = true;
+                        const int Xm = (in_g && ge < Lm) ? dist(um) : Am;
+                        const bool decA = in_g && ge < Lm && Xm != Am, incT = in_g && ge < Lm && Xm != Tm;
+                        const bool gml = in_g && ge == 0 && gamm;
+                        const bool hN = nb_m && nfn_m != old_m, hS = in_g && ge == 0 && nf_af != nf_bf;
+                        const int pA = min(Am, Xm) * p.k + max(Am, Xm), pT = min(Tm, Xm) * p.k + max(Tm, Xm);
+                        int r0 = 2, r1 = 2, r2 = 2, r3 = 2, i0 = 1, i1 = 1;
+                        if (decA) r0 = atomicSub(&mcnt[pA], 1);
+                        if (gml) r1 = atomicSub(&ngk[Am], 1);
+                        if (hN) r2 = atomicSub(&nfh[old_m], 1);
+                        if (hS) r3 = atomicSub(&nfh[nf_bf], 1);
+                        if (incT) i0 = atomicAdd(&mcnt[pT], 1);
+                        if (gml) i1 = atomicAdd(&ngk[Tm], 1);
+                        if (hN) atomicAdd(&nfh[nfn_m], 1);
+                        if (hS) atomicAdd(&nfh[nf_af], 1);
+                        bool risk = r0 == 1 || r1 == 1 || i0 == 0 || i1 == 0;
+                        if (p.wdyn)
+                            risk = risk || (hN && (nfn_m > wcap || (old_m == wcap && r2 == 1))) ||
+                                   (hS && (nf_af > wcap || (nf_bf == wcap && r3 == 1)));
+                        if (__any(risk)) {
+                            FC_PROF(20, 1);
+                            if (decA) atomicAdd(&mcnt[pA], 1);
+                            if (gml) atomicAdd(&ngk[Am], 1);
+                            if (hN) atomicAdd(&nfh[old_m], 1);
+                            if (hS) atomicAdd(&nfh[nf_bf], 1);
+                            if (incT) atomicSub(&mcnt[pT], 1);
+                            if (gml) atomicSub(&ngk[Tm], 1);
+                            if (hN) atomicSub(&nfh[nfn_m], 1);
+                            if (hS) atomicSub(&nfh[nf_af], 1);
+                            compiler_fence();
+                            nA_ = 0;
+                            for (int g = 0; g < nF; ++g) {
+                                bool chg = false;
+                                if (gi == g && ge < Lm) {
+                                    if (decA && atomicSub(&mcnt[pA], 1) == 1) {
+                                        atomicAnd(&adj[Am], ~(1u << Xm));
+                                        atomicAnd(&adj[Xm], ~(1u << Am));
+                                        chg = true;
+                                    }
+                                    if (incT && atomicAdd(&mcnt[pT], 1) == 0) {
+                                        atomicOr(&adj[Tm], 1u << Xm);
+                                        atomicOr(&adj[Xm], 1u << Tm);
+                                        chg = true;
+                                    }
                                 }
-                                if (X != Tm && atomicAdd(&mcnt[min(Tm, X) * p.k + max(Tm, X)], 1) == 0) {
-                                    atomicOr(&adj[Tm], 1u << X);
-                                    atomicOr(&adj[X], 1u << Tm);
-                                    chg = true;
+                                if (gi == g && gml) {
+                                    if (atomicSub(&ngk[Am], 1) == 1) {
+                                        atomicAnd(&adj[Am], ~(1u << 31));
+                                        atomicAnd(&adj[31], ~(1u << Am));
+                                        chg = true;
+                                    }
+                                    if (atomicAdd(&ngk[Tm], 1) == 0) {
+                                        atomicOr(&adj[Tm], 1u << 31);
+                                        atomicOr(&adj[31], 1u << Tm);
+                                        chg = true;
+                                    }
                                 }
-                            }
-                            if (gi == g && ge == 0 && gamm) {
-                                if (atomicSub(&ngk[Am], 1) == 1) {
-                                    atomicAnd(&adj[Am], ~(1u << 31));
-                                    atomicAnd(&adj[31], ~(1u << Am));
-                                    chg = true;
+                                if (gi == g && hN) {
+                                    atomicSub(&nfh[old_m], 1);
+                                    atomicAdd(&nfh[nfn_m], 1);
                                 }
-                                if (atomicAdd(&ngk[Tm], 1) == 0) {
-                                    atomicOr(&adj[Tm], 1u << 31);
-                                    atomicOr(&adj[31], 1u << Tm);
-                                    chg = true;
+                                if (gi == g && hS) {
+                                    atomicSub(&nfh[nf_bf], 1);
+                                    atomicAdd(&nfh[nf_af], 1);
                                 }
-                            }
-                            if (gi == g && nb_m && nfn_m != old_m) {
-                                atomicSub(&nfh[old_m], 1);
-                                atomicAdd(&nfh[nfn_m], 1);
-                            }
-                            if (gi == g && ge == 0 && nf_af != nf_bf) {
-                                atomicSub(&nfh[nf_bf], 1);
-                                atomicAdd(&nfh[nf_af], 1);
-                            }
-                            ++nA_;
-                            adj_chg = __any(chg);
-                            if (p.wdyn) {
-                                compiler_fence();
-                                const uint64_t hm = __ballot(lane >= 1 && lane < kNfh && nfh[lane] > 0);
-                                const int wn = hm ? 63 - __builtin_clzll(hm) : 1;
-                                if (wn != wcap) {
-                                    wcap = wn;
-                                    wthr = (0u - (uint32_t)wcap) % (uint32_t)wcap;
-                                    wcap_chg = true;
+                                ++nA_;
+                                adj_chg = __any(chg);
+                                if (p.wdyn) {
+                                    compiler_fence();
+                                    const uint64_t hm = __ballot(lane >= 1 && lane < kNfh && nfh[lane] > 0);
+                                    const int wn = hm ? 63 - __builtin_clzll(hm) : 1;
+                                    if (wn != wcap) {
+                                        wcap = wn;
+                                        wthr = (0u - (uint32_t)wcap) % (uint32_t)wcap;
+                                        wcap_chg = true;
+                                    }
                                 }
+                                if (adj_chg || wcap_chg) break;
                             }
-                            if (adj_chg || wcap_chg) break;
                         }
+                        FC_STAMP(t_m3);
+                        FC_PROF(25, t_m3 - t_m2);
                         // the flips applied: districts and counts, populations, marks cleared
                         const bool app = gi < nA_;
                         const int pvm = __shfl(pv, mg);
@@ -706,18 +748,29 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                         const bool ent_m = app && nb_m && old_m == 0 && nfn_m > 0;
                         const bool lev_m = app && nb_m && old_m > 0 && nfn_m == 0;
                         // the slots up to the last flip applied: verdict bits, |cut| / |B| after each flip
-                        const int fl = select_bit64(FM, nA_ - 1);
+                        const int fl = nA_ == nF ? f_last : select_bit64(FM, nA_ - 1);
                         if (prop && lane >= f && lane <= fl) st |= bits;
-                        for (int g = 0; g < nA_; ++g) {
-                            const int lg = select_bit64(FM, g);
-                            cut += (int)((rlu(pk3, lg) >> 16) & 0x3fu) - 32;
-                            nb += __popcll(__ballot(ent_m && gi == g)) - __popcll(__ballot(lev_m && gi == g));
-                            if (lane == lg) {
-                                st |= ST_VS | ST_AC;
-                                cut_after = cut;
-                                nb_after = nb;
+                        // flip of rank rk (slot order): |cut| after it = cut + the first rk+1 deltas
+                        // (lane group g holds flip g's delta), |B| = nb + the entering / leaving
+                        // neighbours of lane groups 0..rk
+                        const int rk = count_below(FM);
+                        const int dm = (int)((pk3m >> 16) & 0x3fu) - 32;
+                        int csum = 0, my_cs = 0;
+#pragma unroll
+                        for (int g = 0; g < kGrp; ++g)
+                            if (g < nA_) {
+                                csum += rl32(dm, g * RMAX);
+                                my_cs = rk == g ? csum : my_cs;
                             }
+                        const uint64_t ENT = __ballot(ent_m), LEV = __ballot(lev_m);
+                        if (((FM >> lane) & 1ull) && rk < nA_) {
+                            const uint64_t upto = bits_below((rk + 1) * RMAX);
+                            st |= ST_VS | ST_AC;
+                            cut_after = cut + my_cs;
+                            nb_after = nb + __popcll(ENT & upto) - __popcll(LEV & upto);
                         }
+                        cut += csum;
+                        nb += __popcll(ENT) - __popcll(LEV);
                         rem -= __popcll(VAL & lane_range(f, fl + 1));
                         last_flip = rl32(v, fl);
                         compiler_fence();
@@ -736,6 +789,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                             if (e2 < end) end = e2;
                         }
                         pos = fl + 1;
+                        FC_STAMP(t_m4);
+                        FC_PROF(26, t_m4 - t_m3);
                         continue;
                     }
                 }

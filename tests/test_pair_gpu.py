@@ -327,23 +327,29 @@ def test_packed_node_bytes_saturated_counts(gpu, cref, chunks):
     _check(cref, spec, run, k, inits, bases, steps=3000, pct=0.9)
 
 
-@pytest.mark.parametrize("case", ["c3_tight", "c4", "c5"])
+@pytest.mark.parametrize("case", ["c3_tight", "c4", "c5", "grid_small"])
 def test_multi_flip_commit_equals_one_at_a_time(gpu, cref, sec11, case):
     """The district-rule instance commits several independent accepted flips per pass
     (fc_params.tune_multi_flip; auto = on for graphs of >= 4096 nodes, forced on here): traced
     per proposal against the oracle, and its
     lean instance state for state against one flip at a time.  c3_tight: sec11 k = 4 with a 1 %
     population tolerance (population verdicts change under the flips taken before them); c4 /
-    c5: the triangular lattice and the Delaunay graph, always-accept base 1 among the bases."""
+    c5: the triangular lattice and the Delaunay graph, always-accept base 1 among the bases;
+    grid_small: nine districts of 16 cells, whose adjacencies and slot bound move often, so the
+    pass's all-at-once district-table update falls back to one flip at a time (tools/mf_cover.py
+    counts those passes with the FC_PHASE_PROF build)."""
     if case == "c3_tight":
         spec, k, pct, steps = sec11, 4, 0.01, 2000
         a0 = spec.assignment_array(G.quadrant_plan(spec.nodes), list(range(k)))
     elif case == "c4":
         spec, k, pct, steps = G.triangular_graph(40, 78), 8, 0.1, 2000
         a0 = spec.assignment_array(G.strip_plan(spec, k), list(range(k)))
-    else:
+    elif case == "c5":
         spec, k, pct, steps = G.delaunay_graph(2000, seed=0), 18, 0.1, 2000
         a0 = spec.assignment_array(G.bisection_plan(spec, k), list(range(k)))
+    else:
+        spec, k, pct, steps = G.grid_graph(12, 12), 9, 0.9, 3000
+        a0 = spec.assignment_array(G.strip_plan(spec, k), list(range(k)))
     inits = np.stack([a0] * 12)
     bases = np.asarray([1.0, 0.5, 2.0, 1.0] * 3)
     run = _run_pair(spec, inits, bases, k, steps=steps, pct=pct, chunks=2, tune={"multi_flip": 1})

@@ -20,4 +20,8 @@ for g in range(G):
           f"  slot-bound change {x[16] / b:.3f}")
     if S >= 28 and x[21] > 0:
         print(f"  multi-flip passes {x[21] / b:.2f} per batch, flips per pass {x[22] / max(x[21], 1):.2f}"
-              f" ({x[22] / fl:.2f} of the flips)")
+              f" ({x[22] / fl:.2f} of the flips), fallbacks {x[27] / max(x[21], 1):.2f} per pass,"
+              f" one-by-one table passes {x[20] / max(x[21] - x[27], 1):.3f}")
+        print(f"  multi-flip cycles per pass: members {x[23] / x[21]:.0f}  recount+entering {x[24] / x[21]:.0f}"
+              f"  district tables (sequential) {x[25] / max(x[21] - x[27], 1):.0f}"
+              f"  apply tail {x[26] / max(x[21] - x[27], 1):.0f}")
