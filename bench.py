@@ -157,8 +157,10 @@ class Workload:
         return self._plans[self.plan_of(g)]
 
 
-LDS_GRANULE = 2048  # measured: a workgroup's LDS is allocated in 2 KiB steps (C4, 12,944 B per chain:
-                   # 11 one-wave workgroups per CU are resident, a 12th waits: 41.1 against 55.5 ms)
+LDS_GRANULE = 1280  # measured: a workgroup's LDS is allocated in 1280 B steps (C4, 12,944 B per chain:
+                   # 11 one-wave workgroups per CU are resident, a 12th waits: 41.1 against 55.5 ms;
+                   # C5 at 13,872 B holds 11 per CU, at 14,128 B only 10: 56.5 against 77.0 ms.
+                   # 2048 B fits the first, not the second; 1280 B = 160 KiB / 128 fits both)
 
 
 def resident_chains(fg, W, device: int = 0) -> int:

@@ -373,7 +373,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
                           // rule), thresholds, [BFS scratch | district tables], slots, district
                           // populations, wait queue
         r->chain_lds_bytes = (r->dgraph ? 1 : 2) * r->npad + (2 * R + 2) * 8 +
-                             (r->dgraph ? fc::dgraph_lds_bytes(k) + (R == 8 ? 256 : 0) : fc::bfs_bytes(n)) +
+                             (r->dgraph ? fc::dgraph_lds_bytes(k) + fc::hb_bytes(R) : fc::bfs_bytes(n)) +
                              5 * 64 * 4 + fc::kMaxKGeneral * 4 + fc::kNfh * 4 + fc::kWaitQK * 16;
     // PAIR slot bound: fc_params.wmax > 0 fixes it; otherwise the canonical stream's bound is
     // the state's largest foreign-district count (kept on the device, r->wmax = 0)
@@ -409,12 +409,11 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         if (t.hit_stop < 1) return fail(FC_ERR_ARG, "fc_run_create: tune_hit_stop must be >= 1");
         t.par_min = p->tune_par_min ? p->tune_par_min : 3;
         if (t.par_min < 1) return fail(FC_ERR_ARG, "fc_run_create: tune_par_min must be >= 1");
-        // k > 2 with the district-graph rule on RMAX = 8 rings: commit several independent flips
-        // per pass.  Auto (0): on for graphs of >= 4096 nodes, whose batches' flips rarely share
-        // a ring (C4 +8 %); off on small ones, where they often do (C3: -9 %)
+        // k > 2 with the district-graph rule: commit several independent flips per pass (64 /
+        // RMAX of them).  Auto (0) = on (C4 +32 %, C3 +3.5 %)
         if (p->tune_multi_flip < -1 || p->tune_multi_flip > 1)
             return fail(FC_ERR_ARG, "fc_run_create: tune_multi_flip must be 0 (auto), 1 (on) or -1 (off)");
-        t.multi = p->tune_multi_flip == 1 || (p->tune_multi_flip == 0 && n >= 4096);
+        t.multi = p->tune_multi_flip != -1;
         const int qmax = k == 2 ? fc::kWaitQ : fc::kWaitQK;
         t.wait_q = p->tune_wait_queue ? p->tune_wait_queue : qmax;
         if (t.wait_q < 1 || t.wait_q > qmax)

@@ -22,6 +22,8 @@ constexpr int kMaxKGeneral = 32;    // districts of the general (PAIR) kernel
 constexpr int kMaxKDistrictRule = 31;  // district-graph rule: bit 31 of a district mask is the outer face
 // LDS bytes of the district-graph rule's per-chain tables: pair counts, adjacency masks, outer counts
 inline int dgraph_lds_bytes(int k) { return 4 * k * k + 4 * 32 + 4 * 32; }
+// the multi-flip commit's hashed neighbour marks (fc_kernels.hip), after the district tables
+constexpr int hb_bytes(int ring_max) { return ring_max == 8 ? 256 : 128; }
 
 // meta word layout (also exported by fc_graph_rings)
 constexpr uint64_t kMetaLenMask = 0xffull;
@@ -168,7 +170,7 @@ constexpr int kDealKeys = 1 << 15;
 // slots: 0 loop total, 1 draws, 2 evaluate, 3 commit, 4 bookkeeping, 5 batches,
 //        6 commit-loop iterations, 7 applied flips; k = 2 commit detail: 8 verdicts,
 //        9 one-event classify, 10 one-event apply, 11 segment-parallel, 12 segments
-constexpr int kProfSlots = 28;
+constexpr int kProfSlots = 32;
 // k = 2 lean kernel: accepted states queued for their geometric wait (fc_flip2.hip wait_flush)
 constexpr int kWaitQ = 64;
 // k > 2 kernel: 32 entries, so that sec11 chains keep four waves per SIMD in 160 KB of LDS

@@ -47,8 +47,8 @@ using namespace dev;
 // RMAX = 8: at most 128 VGPRs, four waves per SIMD (C3's 8192 chains per GPU run in two
 // rounds of waves instead of three: 1.46e9 against 1.35e9 proposals/s; a handful of VGPRs
 // spill, which costs C4's LDS-limited launch 2 %)
-// MF (KM = 3, RMAX = 8 only): the multi-flip commit below, in an instance of its own so that
-// runs without it keep the smaller code
+// MF (KM = 3): the multi-flip commit below, in an instance of its own so that runs without it
+// keep the smaller code
 template <int RMAX, int NSUB, int KM, bool FULL, bool MF>
 __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -102,9 +102,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     uint32_t *adj = (uint32_t *)(mcnt + p.k * p.k);
     int32_t *ngk = (int32_t *)(adj + 32);
     const bool dgraph = KM == 3 || (KM != 2 && p.dgraph != 0);  // KM = 3: always, by construction
-    // KM = 3 multi-flip commit: marks of the members' neighbours, hashed to 2048 bits (a
-    // collision only ends a group early)
+    // KM = 3 multi-flip commit: marks of the members' neighbours, hashed to 2048 bits (1024 for
+    // RMAX = 16, which keeps C5's chain at 11 LDS granules; a collision only ends a group early)
     uint32_t *hb = (uint32_t *)(ngk + 32);
+    constexpr int kHbMask = fc::hb_bytes(RMAX) * 8 - 1;
     // cooperative search control words (coop implies no district tables: they start here)
     int32_t *ctl = (int32_t *)(q_run + kWaitQK);
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             const int kk = p.k * p.k;
             for (int i = lane; i < kk; i += kWave) mcnt[i] = p.mcnt[(size_t)c * kk + i];
             if (lane < 32) ngk[lane] = p.ngk[(size_t)c * 32 + lane];
-            if (KM == 3 && MF) hb[lane] = 0u;
+            if (KM == 3 && MF && lane < fc::hb_bytes(RMAX) / 4) hb[lane] = 0u;
             wave_sync();
             // adj[X] bit Y: some face holds cells of X and Y; bit 31: X touches the outer face
             uint32_t m = 0;
@@ -543,9 +544,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                     int cutP = kWave;   // first proposal whose population verdict changed
                     int dA = 0, dT = 0; // this slot's district populations moved by the taken flips
                     const int gi = lane / RMAX, ge = lane % RMAX;
-                    for (uint64_t CC = CANDM; CC && nF < kGrp; CC &= CC - 1ull) {
+                    uint64_t CC = CANDM;
+                    for (; CC && nF < kGrp; CC &= CC - 1ull) {
                         const int i = __builtin_ctzll(CC);
-                        if (i >= cutA || i >= cutP) break;
+                        if (i >= cutA || i >= cutP) {
+                            FC_PROF(i >= cutA ? 29 : 30, 1);
+                            break;
+                        }
                         const int vi = rl32(v, i);
                         const uint32_t pki = rlu(pk, i), nbri = rlu(pk2, i) >> 16;
                         const int Ai = (int)((pki >> 15) & 63u), Ti = (int)((pki >> 21) & 63u);
@@ -560,16 +565,20 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                         const int ui = (int)((sel >> (16 * (ge & 1))) & 0xffffu);
                         const bool isn = gi == 0 && ((nbri >> ge) & 1u);
                         if (nF > 0) {
-                            const bool clash = isn && ((hb[(ui & 2047) >> 5] >> (ui & 31)) & 1u);
-                            if (__any(clash)) break;
+                            const bool clash = isn && ((hb[(ui & kHbMask) >> 5] >> (ui & 31)) & 1u);
+                            if (__any(clash)) {
+                                FC_PROF(31, 1);
+                                break;
+                            }
                         }
-                        if (isn) atomicOr(&hb[(ui & 2047) >> 5], 1u << (ui & 31));
+                        if (isn) atomicOr(&hb[(ui & kHbMask) >> 5], 1u << (ui & 31));
                         FM |= 1ull << i;
                         ++nF;
-                        // later slots whose node is vi or in its ring (rings are symmetric)
+                        // later slots whose node is vi or has vi in its own ring (rings are symmetric)
                         bool stl = v == vi;
 #pragma unroll
-                        for (int k = 0; k < RMAX; ++k) stl |= v == (int)((rwi[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+                        for (int k2 = 0; k2 < RMAX / 2; ++k2)
+                            stl |= (rec.ring[k2] & 0xffffu) == (uint32_t)vi || (rec.ring[k2] >> 16) == (uint32_t)vi;
                         const uint64_t SM = __ballot(stl && has && lane > i && lane < end);
                         if (SM && __builtin_ctzll(SM) < cutA) cutA = __builtin_ctzll(SM);
                         // the populations of later slots' districts after this flip
@@ -579,6 +588,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                         const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
                         if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
                     }
+                    if (CC && nF == kGrp) FC_PROF(28, 1);
                     FC_STAMP(t_m1);
                     FC_PROF(23, t_m1 - t_m0);
                     const int f_last = 63 - __builtin_clzll(FM);
@@ -641,7 +651,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                         FC_PROF(27, 1);
                         // not worth it, or the launch's last step / an entering draw lies inside:
                         // clear the marks and take f alone
-                        if (nb_m) hb[(um & 2047) >> 5] = 0u;
+                        if (nb_m) hb[(um & kHbMask) >> 5] = 0u;
                         compiler_fence();
                     } else {
                         // district tables and nf histogram: all flips at once, decrements before
@@ -738,7 +748,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                         // the flips applied: districts and counts, populations, marks cleared
                         const bool app = gi < nA_;
                         const int pvm = __shfl(pv, mg);
-                        if (nb_m) hb[(um & 2047) >> 5] = 0u;
+                        if (nb_m) hb[(um & kHbMask) >> 5] = 0u;
                         if (app && ge == 0) {
                             pkb[vm] = (uint8_t)(Tm | ((nf_af < 7 ? nf_af : 7) << 5));
                             atomicSub(&popk[Am], pvm);
@@ -1307,10 +1317,10 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, siz
                      M ? ", true" : "");                                                                \
         hipLaunchKernelGGL((flip_kernel<R, S, K, F, M>), grid, block, lds, s, p);                       \
     } while (0)
-    // the multi-flip instance: district-graph rule, RMAX = 8, when the run asks for it
+    // the multi-flip instance: district-graph rule, when the run asks for it
 #define FC_LAUNCH(R, S, K, F)                                                     \
     do {                                                                          \
-        if (K == 3 && R == 8 && p.multi_flip) FC_LAUNCHM(R, S, K, F, (K == 3 && R == 8)); \
+        if (K == 3 && p.multi_flip) FC_LAUNCHM(R, S, K, F, (K == 3));         \
         else FC_LAUNCHM(R, S, K, F, false);                                        \
     } while (0)
 #define FC_FULL_SWITCH(R, S, K)                          \

@@ -176,9 +176,9 @@ typedef struct fc_params {
      * S into b_nodes, S is rebuilt from that state.  Short boundaries then waste few draws.
      * k = 2, n <= 4096, no replay tape; oracle: fr_params.stream                               */
     int32_t stream;
-    int32_t tune_multi_flip;    /* k > 2 with the district-graph rule, rings of <= 8 cells: commit
-                                   several independent accepted flips per pass (0: auto = on for
-                                   graphs of >= 4096 nodes; 1: on; -1: one at a time).
+    int32_t tune_multi_flip;    /* k > 2 with the district-graph rule: commit several independent
+                                   accepted flips per pass (0: auto = on; 1: on; -1: one at a
+                                   time).
                                    Scheduling only, like every tune_* field                    */
 } fc_params;
 

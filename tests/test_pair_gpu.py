@@ -330,7 +330,7 @@ def test_packed_node_bytes_saturated_counts(gpu, cref, chunks):
 @pytest.mark.parametrize("case", ["c3_tight", "c4", "c5", "grid_small"])
 def test_multi_flip_commit_equals_one_at_a_time(gpu, cref, sec11, case):
     """The district-rule instance commits several independent accepted flips per pass
-    (fc_params.tune_multi_flip; auto = on for graphs of >= 4096 nodes, forced on here): traced
+    (fc_params.tune_multi_flip; auto = on, forced on here): traced
     per proposal against the oracle, and its
     lean instance state for state against one flip at a time.  c3_tight: sec11 k = 4 with a 1 %
     population tolerance (population verdicts change under the flips taken before them); c4 /
@@ -355,8 +355,7 @@ def test_multi_flip_commit_equals_one_at_a_time(gpu, cref, sec11, case):
     run = _run_pair(spec, inits, bases, k, steps=steps, pct=pct, chunks=2, tune={"multi_flip": 1})
     name = run.kernel_name()
     assert ", 3, " in name, name
-    # the multi-flip instance exists for rings of <= 8 cells (C5's Delaunay rings take 16)
-    assert name.endswith(", true, true>") == (case != "c5"), name  # FULL (traced), multi-flip
+    assert name.endswith(", true, true>"), name  # FULL (traced), multi-flip
     _check(cref, spec, run, k, inits, bases, steps=steps, pct=pct)
     fg = FlipGraph(spec)
     _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)

@@ -28,6 +28,6 @@ for name, (spec, k, pct, plan) in cases.items():
     r.steps(3000)
     print(name, r.kernel_name())
     raw = np.fromfile(out, dtype=np.int64)
-    S = next(s for s in (28, 24) if (raw.size // 12) % s == 0)
+    S = next(s for s in (32, 28, 24) if (raw.size // 12) % s == 0)
     x = raw.reshape(-1, 12, S)[-1].sum(axis=0)
     print(f"  passes {x[21]}  not taken {x[27]}  one-by-one tables {x[20]}  flips in passes {x[22]}  flips {x[7]}")

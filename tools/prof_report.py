@@ -6,7 +6,7 @@ import numpy as np
 f, C = sys.argv[1], int(sys.argv[2])
 G = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 raw = np.fromfile(f, dtype=np.int64)
-S = next(k for k in (28, 24, 16, 8) if (raw.size // C) % k == 0)
+S = next(k for k in (32, 28, 24, 16, 8) if (raw.size // C) % k == 0)
 rec = raw.reshape(-1, C, S)
 last = rec[-1].astype(np.float64)
 names = ["total", "draws", "eval", "commit", "book", "batches", "commit_it", "applied"]

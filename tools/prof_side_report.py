@@ -6,7 +6,7 @@ import numpy as np
 
 raw = np.fromfile(sys.argv[1], dtype=np.int64)
 C, G = int(sys.argv[2]), int(sys.argv[3]) if len(sys.argv) > 3 else 1
-S = next(k for k in (28, 24) if (raw.size // C) % k == 0)  # fc_internal.h kProfSlots
+S = next(k for k in (32, 28, 24) if (raw.size // C) % k == 0)  # fc_internal.h kProfSlots
 last = raw.reshape(-1, C, S)[-1].astype(np.float64)
 for g in range(G):
     x = last[np.arange(C) % G == g].mean(axis=0)
@@ -25,3 +25,6 @@ for g in range(G):
         print(f"  multi-flip cycles per pass: members {x[23] / x[21]:.0f}  recount+entering {x[24] / x[21]:.0f}"
               f"  district tables (sequential) {x[25] / max(x[21] - x[27], 1):.0f}"
               f"  apply tail {x[26] / max(x[21] - x[27], 1):.0f}")
+    if S >= 32 and x[21] > 0:
+        print(f"  member selection ends per pass: cap {x[28] / x[21]:.2f}  stale view {x[29] / x[21]:.2f}"
+              f"  population {x[30] / x[21]:.2f}  shared neighbour {x[31] / x[21]:.2f}")
