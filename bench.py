@@ -15,8 +15,11 @@ reference run, ``total_steps=100000`` at ``grid_chain_sec11.py:342``; 10 timed s
 1e6 steps per chain of BASELINE config C2).  Inputs are resident in HBM before the
 timed region; the timed region is bracketed by barrier + device synchronisation.
 
-N > 1 (``torch.distributed.run``): one process per GPU, chains sharded by global id with
-no data-path collective (weak scaling); one RCCL all-reduce of the statistics at the end.
+N > 1: one process per GPU, chains sharded by global id with no data-path collective (weak
+scaling); one RCCL all-reduce of the statistics at the end.  Under ``torch.distributed.run``
+the ranks come from the environment and ``--gpus`` must equal ``WORLD_SIZE``; run directly
+(``python bench.py --gpus N``) the script launches the N ranks itself, before any GPU call, and
+exits with the first failing rank's status.
 """
 from __future__ import annotations
 
@@ -179,6 +182,51 @@ def resident_chains(fg, W, device: int = 0) -> int:
     return cus * max(1, min(160 * 1024 // lds, 16))
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return int(so.getsockname()[1])
+
+
+def launch_ranks(gpus: int) -> int:
+    """``python bench.py --gpus N`` without a launcher: start N ranks of this script (one
+    process per GPU, ``RANK`` = ``LOCAL_RANK`` = r, rendezvous on 127.0.0.1) and wait for them.
+    Runs before anything touches the GPU (the parent never does); a rank that fails ends the
+    others (their exact PIDs), and the first failing status is returned.  Rank 0 prints the
+    line."""
+    import subprocess
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    procs = []
+    for r in range(gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FC_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for pr in list(live):
+            rc = pr.poll()
+            if rc is None:
+                continue
+            live.remove(pr)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                for other in live:
+                    other.terminate()
+    return status
+
+
+def check_world(gpus: int):
+    """``--gpus`` against the launcher's ``WORLD_SIZE``: None when they agree (or no launcher
+    is involved), else the message to exit with."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None and int(ws) != gpus:
+        return f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}: the launcher and the request disagree"
+    return None
+
+
 def _dist():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws <= 1:
@@ -188,9 +236,27 @@ def _dist():
     # FC_BENCH_BACKEND / FC_BENCH_DEVICE only serve rehearsals of the N > 1 path on a
     # one-GPU box (several ranks on device 0 over gloo); the real run uses RCCL, one GPU per rank.
     backend = os.environ.get("FC_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-    dist.init_process_group(backend=backend)
     local = int(os.environ.get("FC_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:
+        raise SystemExit(f"bench.py: rank {os.environ.get('RANK')} wants device {local} but {ndev} are visible "
+                         "(FC_BENCH_DEVICE=0 + FC_BENCH_BACKEND=gloo rehearse several ranks on one GPU)")
+    dist.init_process_group(backend=backend)
     return dist, dist.get_rank(), dist.get_world_size(), local
+
+
+def spawn_probe():
+    """FC_BENCH_SPAWN_PROBE=1 (CPU test of the launcher, tests/test_bench_launch.py): each rank
+    joins the process group over gloo, sums its rank, and rank 0 prints what it saw."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group(backend="gloo")
+    t = torch.tensor([float(dist.get_rank())])
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"ranks_seen": dist.get_world_size(), "rank_sum": float(t.item()),
+                          "launcher": os.environ.get("FC_BENCH_LAUNCHER", "external")}), flush=True)
+    dist.destroy_process_group()
 
 
 def _cpu_worker(args):
@@ -336,9 +402,24 @@ def main():
     ap.add_argument("--tune", default="",
                     help="launch tuning, e.g. nsub=2,hit_stop=24,prio_div=2:5:10 (fc_params.tune_*; "
                          "scheduling only)")
+    ap.add_argument("--allow-variant", action="store_true",
+                    help="load a profiling / experiment library (FC_LIB_PATH, FC_LIB_VARIANT): A/B tools only; "
+                         "the line records fc_build_flags")
     args = ap.parse_args()
 
+    bad = check_world(args.gpus)
+    if bad:
+        print(bad, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if os.environ.get("FC_BENCH_SPAWN_PROBE") == "1":
+        spawn_probe()
+        return
+
     dist, rank, world, local_rank = _dist()
+    from flipcomplexityempirical_amd import _lib as _lib0
+    _lib0.load(allow_variant=args.allow_variant)
     import torch
     from flipcomplexityempirical_amd import graphs as G
     from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune, pin_host, unpin_host
@@ -401,6 +482,10 @@ def main():
     delta = {k: s1[k] - s0[k] for k in D.AGG_FIELDS}
     nb_ = len(W.bases)
     agg = D.allreduce_sum(D.group_aggregate(delta, gids % nb_, nb_), dist, dev)
+    # per-rank record: each rank's mean launch time and timed-region wall time
+    rank_rec = np.zeros((2, world), dtype=np.float64)
+    rank_rec[:, rank] = (kernel_ms, elapsed)
+    rank_rec = D.allreduce_sum(rank_rec, dist, dev)
     elapsed = D.allreduce_max(elapsed, dist, dev)
     kernel_ms = D.allreduce_max(kernel_ms, dist, dev)
     props, steps, acc = (float(agg[:, D.AGG_FIELDS.index(k)].sum()) for k in ("proposals", "steps", "accepted"))
@@ -486,7 +571,7 @@ def main():
         barrier_sync_f()
         f0 = rf.stats()
         rf.timings()
-        t_series, n_events, n_nan, n_changes = 0.0, 0, 0, 0
+        t_series, n_events, n_nan, n_changes, n_cp_fallback = 0.0, 0, 0, 0, 0
         t_pe, n_pe = 0.0, 0   # the per-event form, measured on the last launch only (outside the rates)
         t_acf, acf_out = 0.0, None
         fs_buf = None
@@ -512,6 +597,9 @@ def main():
                 # copy per array into pinned host buffers reused over the launches
                 ch = rf.frame_series_changes(frame, out=cp_buf)
                 n_changes += int(ch["offsets"][-1])
+                # more change points than the pinned buffers hold: a second native call into
+                # fresh unpinned arrays (counted)
+                n_cp_fallback += int(ch["offsets"][-1] > cp_buf["t"].size)
                 n_events += int(rf.stats()["events"].sum())
                 n_nan += int(np.isnan(ch["angle"]).sum())
                 t_series += time.perf_counter() - ts
@@ -561,6 +649,8 @@ def main():
                              + " (the reference loop body, grid_chain_sec11.py:367-400)"),
                     "frame_series": {"ms_per_launch": t_series / max(n_full, 1) * 1e3,
                                      "events": n_events, "change_points": n_changes,
+                                     "pinned_buffer_misses": n_cp_fallback,
+                                     "pinned_buffer_entries": int(cp_buf["t"].size) if cp_buf else None,
                                      "events_per_s": n_events / t_series if t_series else None,
                                      "nan_angles_at_change_points": n_nan,
                                      "note": "fc_run_frame_series_changes over all chains after every launch: the "
@@ -624,6 +714,12 @@ def main():
         "value": value, "unit": "proposals/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "ranks_seen": dist.get_world_size() if dist is not None else 1,
+        "backend": dist.get_backend() if dist is not None else None,
+        "launcher": os.environ.get("FC_BENCH_LAUNCHER") or ("torch.distributed.run" if dist is not None else None),
+        "per_rank_kernel_ms": [float(x) for x in rank_rec[0]],
+        "per_rank_elapsed_s": [float(x) for x in rank_rec[1]],
+        "build_flags": _lib.build_flags(),
         "data": W.data + (" (band node stream: draws over b_nodes + neighbours)" if stream == "band" else ""),
         "config": {"workload": W.desc, "graph": args.workload, "k": W.k, "chains_per_gpu": C,
                    "chain_steps_per_launch": args.chain_steps,

@@ -39,8 +39,12 @@ EXPORTED = [
     "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
     "fc_run_frame_series", "fc_run_frame_series_changes", "fc_host_register", "fc_host_unregister",
     "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_destroy",
-    "fc_device_count", "fc_last_error",
+    "fc_device_count", "fc_last_error", "fc_build_flags",
 ]
+
+FC_BUILD_PHASE_PROF, FC_BUILD_PHASE_SYNC, FC_BUILD_VARIANT = 0x1, 0x2, 0x4  # include/flipchain.h
+# environment variables that select a non-product library (build.py / load below)
+VARIANT_ENV = ("FC_LIB_PATH", "FC_LIB_VARIANT", "FC_HIPCC_FLAGS", "FC_LIB_OUT")
 
 
 class GraphInfo(ctypes.Structure):
@@ -105,17 +109,35 @@ class FlipChainError(RuntimeError):
 
 
 _lib = None
+_allow_variant = False
 
 
 def lib_path() -> str:
     return _build.LIB
 
 
-def load(build_if_missing: bool = True):
-    """Load (building if needed) the native library; raises when it cannot be had."""
-    global _lib
+def build_flags() -> int:
+    """``fc_build_flags()`` of the loaded library (FC_BUILD_*; 0 = the product build)."""
+    return int(load().fc_build_flags())
+
+
+def load(build_if_missing: bool = True, allow_variant: bool = False):
+    """Load (building if needed) the native library; raises when it cannot be had.
+
+    A profiling / experiment library -- selected by FC_LIB_PATH, FC_LIB_VARIANT, FC_HIPCC_FLAGS
+    or FC_LIB_OUT, or reporting FC_BUILD_* bits from ``fc_build_flags()`` -- is refused unless
+    ``allow_variant`` (the A/B and profiling tools pass it; tests, ``bench.py`` and
+    ``smoke()`` do not), so a stray environment variable cannot put a non-product library
+    under the product's loader.  Once allowed, later calls return the same library."""
+    global _lib, _allow_variant
+    if allow_variant:
+        _allow_variant = True
     if _lib is not None:
         return _lib
+    env = [k for k in VARIANT_ENV if os.environ.get(k)]
+    if env and not _allow_variant:
+        raise ImportError(f"libflipchain: {', '.join(env)} set: a variant library is loaded only with "
+                          "_lib.load(allow_variant=True) (A/B and profiling tools)")
     # FC_LIB_PATH: load this prebuilt library as is (A/B timing of two builds on one box)
     path = os.environ.get("FC_LIB_PATH") or _build.LIB
     if build_if_missing and "FC_LIB_PATH" not in os.environ and (not os.path.exists(path) or _build._stale()):
@@ -173,10 +195,16 @@ def load(build_if_missing: bool = True):
     L.fc_device_count.argtypes = [_P(i32)]
     L.fc_last_error.argtypes = []
     L.fc_last_error.restype = ctypes.c_char_p
+    L.fc_build_flags.argtypes = []
+    L.fc_build_flags.restype = ctypes.c_uint32
     for name in EXPORTED:
         if name not in ("fc_graph_destroy", "fc_run_destroy", "fc_last_error", "fc_run_n_chains",
-                        "fc_run_chain_lds_bytes"):
+                        "fc_run_chain_lds_bytes", "fc_build_flags"):
             getattr(L, name).restype = ctypes.c_int
+    bf = int(L.fc_build_flags())
+    if bf and not _allow_variant:
+        raise ImportError(f"{path}: a variant build (fc_build_flags() = {bf:#x}); loaded only with "
+                          "_lib.load(allow_variant=True)")
     _lib = L
     return L
 

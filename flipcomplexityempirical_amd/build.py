@@ -13,13 +13,12 @@ from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
-# FC_LIB_VARIANT selects a diagnostic build: "_"-separated tokens, each a -D flag
-# (prof: per-phase s_memtime counters; sync: each stamp drains outstanding memory first).
+# FC_LIB_VARIANT selects a diagnostic build under its own file name: "_"-separated tokens, each a
+# -D flag (prof: per-phase s_memtime counters; sync: each stamp drains outstanding memory first).
+# Such a build (and any with FC_HIPCC_FLAGS) also gets -DFC_VARIANT_BUILD: fc_build_flags()
+# reports it and _lib.load() refuses it unless called with allow_variant=True (tools only).
 VARIANT = os.environ.get("FC_LIB_VARIANT", "")
-VARIANT_FLAGS = {"prof": "-DFC_PHASE_PROF", "sync": "-DFC_PHASE_SYNC", "mask": "-DFC_MASKED_STORES",
-                 "dupnf": "-DFC_EXP_DUP_NF", "dupdg": "-DFC_EXP_DUP_DG",
-                 "dupdraw": "-DFC_EXP_DUP_DRAW", "dupeval": "-DFC_EXP_DUP_EVAL", "dupmarks": "-DFC_EXP_DUP_MARKS",
-                 "dupapply": "-DFC_EXP_DUP_APPLY"}
+VARIANT_FLAGS = {"prof": "-DFC_PHASE_PROF", "sync": "-DFC_PHASE_SYNC"}
 LIB = os.environ.get("FC_LIB_OUT") or os.path.join(PKG, f"libflipchain_{VARIANT}.so" if VARIANT else "libflipchain.so")
 SOURCES = ["fc_flip2.hip", "fc_deal.hip", "fc_kernels.hip", "fc_series.hip", "fc_recom.hip", "fc_capi.cpp", "fc_graph.cpp"]
 HEADERS = ["fc_internal.h", "fc_philox.h", "fc_device.h", "fc_ring.h", os.path.join("..", "..", "include", "flipchain.h")]
@@ -52,9 +51,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
     for tok in filter(None, VARIANT.split("_")):
+        if tok not in VARIANT_FLAGS:
+            raise ValueError(f"FC_LIB_VARIANT token {tok!r} (known: {', '.join(VARIANT_FLAGS)})")
         flags.append(VARIANT_FLAGS[tok])
     # FC_HIPCC_FLAGS: extra compiler flags for experiment builds (with FC_LIB_OUT naming the output)
-    flags += os.environ.get("FC_HIPCC_FLAGS", "").split()
+    extra = os.environ.get("FC_HIPCC_FLAGS", "").split()
+    flags += extra
+    if VARIANT or extra:
+        flags.append("-DFC_VARIANT_BUILD")
     with tempfile.TemporaryDirectory(prefix="fc_build_") as tmp:
         objs = [os.path.join(tmp, os.path.splitext(src)[0] + ".o") for src in SOURCES]
         jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(SOURCES), os.cpu_count() or 1, 8)

@@ -794,21 +794,26 @@ class ChainResult:
 
     @classmethod
     def from_run(cls, chain: MarkovChain, run, c: int) -> "ChainResult":
-        sp, lab = chain.cspec.spec, chain.cspec.labels
         st = run.stats()
         ch, nh = run.hist()
-        ct = run.cut_times()[c]
         nf, ps, lf = run.flips()
-        fin = run.state()[c]
-        e = chain.edges
+        return cls.from_arrays(chain.cspec, chain.edges, st, ch, nh, run.cut_times(), nf, ps, lf, run.state(), c)
+
+    @classmethod
+    def from_arrays(cls, cspec, edges, st, ch, nh, ct, nf, ps, lf, fin, c: int) -> "ChainResult":
+        """Chain ``c`` of a run's read-outs (``stats``, ``hist``, ``cut_times``, ``flips``,
+        ``state``, each ``[chains, ...]``): the one place a ChainResult is assembled, for the
+        single-chain ``MarkovChain.run`` and the batched ``sweep.Sweep`` alike."""
+        sp, lab = cspec.spec, cspec.labels
+        ctc, finc = ct[c], fin[c]
         return cls(
             steps=int(st["steps"][c]), proposals=int(st["proposals"][c]), accepted=int(st["accepted"][c]),
             waits_sum=int(st["sum_wait"][c]), rce_sum=int(st["sum_cut"][c]), rbn_sum=int(st["sum_nb"][c]),
             cut_hist=ch[c], nb_hist=nh[c],
-            cut_times={(sp.nodes[u], sp.nodes[v]): int(ct[i]) for i, (u, v) in enumerate(e)},
+            cut_times={(sp.nodes[u], sp.nodes[v]): int(ctc[i]) for i, (u, v) in enumerate(edges)},
             num_flips={sp.nodes[i]: int(nf[c, i]) for i in range(sp.n)},
             part_sum={sp.nodes[i]: int(ps[c, i]) for i in range(sp.n)},
             last_flipped={sp.nodes[i]: int(lf[c, i]) for i in range(sp.n)},
             lognum_flips={sp.nodes[i]: math.log(int(nf[c, i]) + 1) for i in range(sp.n)},
-            final_assignment={sp.nodes[i]: lab[fin[i]] for i in range(sp.n)},
+            final_assignment={sp.nodes[i]: lab[finc[i]] for i in range(sp.n)},
             stats={k: int(v[c]) for k, v in st.items()})

@@ -183,6 +183,20 @@ extern "C" {
 
 const char *fc_last_error(void) { return g_err.c_str(); }
 
+uint32_t fc_build_flags(void) {
+    uint32_t f = 0;
+#ifdef FC_PHASE_PROF
+    f |= FC_BUILD_PHASE_PROF;
+#endif
+#ifdef FC_PHASE_SYNC
+    f |= FC_BUILD_PHASE_SYNC;
+#endif
+#ifdef FC_VARIANT_BUILD
+    f |= FC_BUILD_VARIANT;
+#endif
+    return f;
+}
+
 int fc_device_count(int32_t *n) {
     if (!n) return fail(FC_ERR_ARG, "fc_device_count: null output");
     int c = 0;
@@ -371,9 +385,11 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
                 !(p->flags & FC_FLAG_FORCE_BFS);
     if (!recom && k > 2)  // fc_kernels.hip: a, fcnt (one packed byte per node with the district-graph
                           // rule), thresholds, [BFS scratch | district tables], slots, district
-                          // populations, wait queue
+                          // populations, wait queue; the multi-flip commit's hashed marks (last)
+                          // only when it is on, so an "off" run keeps its residency
         r->chain_lds_bytes = (r->dgraph ? 1 : 2) * r->npad + (2 * R + 2) * 8 +
-                             (r->dgraph ? fc::dgraph_lds_bytes(k) + fc::hb_bytes(R) : fc::bfs_bytes(n)) +
+                             (r->dgraph ? fc::dgraph_lds_bytes(k) + (p->tune_multi_flip != -1 ? fc::hb_bytes(R) : 0)
+                                        : fc::bfs_bytes(n)) +
                              5 * 64 * 4 + fc::kMaxKGeneral * 4 + fc::kNfh * 4 + fc::kWaitQK * 16;
     // PAIR slot bound: fc_params.wmax > 0 fixes it; otherwise the canonical stream's bound is
     // the state's largest foreign-district count (kept on the device, r->wmax = 0)

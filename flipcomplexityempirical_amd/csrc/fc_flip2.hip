@@ -71,16 +71,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     uint8_t *smark = (uint8_t *)(slot + 5 * 64);   // [npad] lowest slot of a segment flip at the node
     uint8_t *nmark = smark + npad;                 // [npad] ... having the node as a neighbour
     uint8_t *const dum = nmark + npad + (lane & 15);  // [16] sink for masked-off stores
-    // a store only some lanes make: FC_MASKED_STORES masks the others off (exec mask), else they
-    // write the sink (no branch, but 64 lanes on 16 bytes)
-#ifdef FC_MASKED_STORES
-#define FC_ST(cond, ref, val) \
-    do {                      \
-        if (cond) (ref) = (val); \
-    } while (0)
-#else
+    // a store only some lanes make: the others write the sink (no branch; storing under exec
+    // masks instead measured no faster, profiles/r03c_ab_masked_stores)
 #define FC_ST(cond, ref, val) (*((cond) ? (uint8_t *)&(ref) : dum) = (uint8_t)(val))
-#endif
     // accepted states whose geometric wait is still to be drawn (kWaitQ of them:
     // creating draw, |B| after the flip, yields so far); see wait_flush below
     uint64_t *q_d = (uint64_t *)(nmark + npad + 16);
@@ -343,22 +336,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + (inrange ? dr : draw)) * 6;
                 w = Words4{t[0], t[1], t[2], t[3]};
             } else {
-#ifdef FC_EXP_CHEAPRNG
-                {  // timing experiment only: a 2-multiply mix instead of Philox (not the canonical stream)
-                    uint64_t z = dr * 0x9E3779B97F4A7C15ull + ((uint64_t)chain_gid << 32) + p.seed_lo;
-                    z = (z ^ (z >> 31)) * 0xBF58476D1CE4E5B9ull;
-                    z ^= z >> 29;
-                    w = Words4{(uint32_t)z, (uint32_t)(z >> 32), (uint32_t)(z >> 16) ^ (uint32_t)dr, 0u};
-                }
-#else
                 w = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
-#ifdef FC_EXP_DUP_DRAW
-                {  // timing experiment only: a second Philox per draw, discarded
-                    const Words4 wx = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 7u, p.seed_lo, p.seed_hi);
-                    asm volatile("" ::"v"(wx.x0 ^ wx.x1 ^ wx.x2 ^ wx.x3));
-                }
-#endif
-#endif
             }
             int vd;
             bool okd;
@@ -415,15 +393,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         int v = has ? (int)slot[lane] : 0;
         const uint32_t w1 = slot[64 + lane], w2 = slot[128 + lane];
         const NodeRec<RMAX> rec = G[v];
-#ifdef FC_EXP_DUP_EVAL
-        {  // timing experiment only: the slot's record and ring districts once more, discarded
-            const NodeRec<RMAX> rx = G[v ^ 0];
-            uint32_t ix = 0;
-#pragma unroll
-            for (int i = 0; i < RMAX; ++i) ix |= (uint32_t)a[ring_entry<RMAX>(rx.ring, i)] << i;
-            asm volatile("" ::"v"(ix));
-        }
-#endif
         int av = a[v];
         int pv = rec.pop;
         const uint32_t Ln = (uint32_t)(rec.meta & kMetaLenMask);
@@ -699,14 +668,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         need = need && again;
                         if (!__any(need)) break;
                     }
-#ifdef FC_EXP_DUP_MARKS
-                    {  // timing experiment only: the marks' reads once more, discarded
-                        int xs = smark[v];
-#pragma unroll
-                        for (int i = 0; i < RMAX; ++i) xs += nmark[cell[i]] + smark[cell[i]];
-                        asm volatile("" ::"v"(xs));
-                    }
-#endif
                     FC_STAMP(t_mk);
                     FC_PROF(18, t_mk - t_it1);
                     bool conf = ms < lane;
@@ -886,12 +847,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             bool enter = false, leave = false, outS = false;
             if (is_nbr) {
                 const int old = fcnt[my_e];
-#ifdef FC_EXP_DUP_APPLY
-                {  // timing experiment only: the neighbour's count read once more, discarded
-                    const int ox = fcnt[my_e ^ 0];
-                    asm volatile("" ::"v"(ox));
-                }
-#endif
                 const uint64_t swd = BAND ? sb[my_e >> 6] : 0ull;
                 fcnt[my_e] = (uint8_t)(old + dlt);
                 enter = dlt > 0 && old == 0;
@@ -1185,13 +1140,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     if (defer && qn > 0) wait_flush();
     FC_STAMP(t_loop1);
     FC_PROF(0, t_loop1 - t_loop0);
-#ifdef FC_EXP_DEAL_TIME
-    if (p.ctime && lane == 0) p.ctime[c] = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - misc[0], (uint64_t)0xffffffffu);
-#else
     // the chain's own work this launch (draws: a short boundary costs many per step), not its
     // duration, which its SIMD-mates stretch
     if (p.ctime && lane == 0) p.ctime[c] = (uint32_t)min(draw - scp->draw, (uint64_t)0xffffffffu);
-#endif
     if (p.eta && rem == 0 && lane == 0) {  // this launch's pace, for the next one's priorities
         const uint64_t el = __builtin_amdgcn_s_memrealtime() - misc[0];
         atomicMax(&p.eta[p.eta_parity], (uint32_t)min(el * 1024ull / (uint64_t)max((int)p.n_steps, 1), 0xffffffffull));

@@ -844,16 +844,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                     else a[vf] = (int8_t)tf;
                 }
                 compiler_fence();
-#ifdef FC_EXP_DUP_NF
-                if (is_nbr) {  // timing experiment only: the recount once more, its result discarded
-                    const NodeRec<RMAX> rx = G[my_e ^ 0];
-                    const uint32_t nbx = (uint32_t)(rx.meta >> kMetaNbrShift) & 0xffffu;
-                    uint32_t dx = 0;
-                    for (int i = 0; i < RMAX; ++i)
-                        if ((nbx >> i) & 1u) dx |= 1u << dist(ring_entry<RMAX>(rx.ring, i));
-                    asm volatile("" ::"v"(dx));
-                }
-#endif
                 if (is_nbr) {
                     const NodeRec<RMAX> ru = G[my_e];
                     const int au = dist(my_e);
@@ -915,15 +905,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             if (dgraph) {
                 const int Lf = rl32((int)Ln, f);
                 bool chg = false;
-#ifdef FC_EXP_DUP_DG
-                if (lane < Lf) {  // timing experiment only: the pair-count atomics once more, adding 0
-                    const int X = dist(my_e);
-                    int o1 = 0, o2 = 0;
-                    if (X != Af) o1 = atomicAdd(&mcnt[min(Af, X) * p.k + max(Af, X)], 0);
-                    if (X != tf) o2 = atomicAdd(&mcnt[min(tf, X) * p.k + max(tf, X)], 0);
-                    asm volatile("" ::"v"(o1), "v"(o2));
-                }
-#endif
                 if (lane < Lf) {
                     const int X = dist(my_e);
                     if (X != Af && atomicSub(&mcnt[min(Af, X) * p.k + max(Af, X)], 1) == 1) {

@@ -186,7 +186,7 @@ typedef struct fc_params {
 #define FC_STREAM_BAND 1
 
 /* Zero *p, then set struct_size / abi_version and the defaults a zeroed struct does not give:
- * base 1, pop bounds [0, INT32_MAX], hitting-time window off.  FC_ERR_ARG when struct_size is
+ * k = 2, base 1, pop bounds [0, INT32_MAX], hitting-time window off.  FC_ERR_ARG when struct_size is
  * not this library's sizeof(fc_params) (the caller's header is another version).            */
 int fc_params_init(fc_params *p, uint32_t struct_size);
 
@@ -388,6 +388,14 @@ void fc_run_destroy(fc_run *r);
 
 int fc_device_count(int32_t *n);
 const char *fc_last_error(void);
+
+/* What this library was built with (FC_BUILD_* bits; 0 = the product build).  A profiling or
+ * experiment build counts phases in the kernels or was compiled with extra flags: its timings
+ * are not the product's, so the Python loader refuses it unless asked (_lib.load(allow_variant)). */
+#define FC_BUILD_PHASE_PROF 0x1u   /* -DFC_PHASE_PROF: per-phase s_memtime counters per chain   */
+#define FC_BUILD_PHASE_SYNC 0x2u   /* -DFC_PHASE_SYNC: each stamp drains outstanding memory     */
+#define FC_BUILD_VARIANT 0x4u      /* built with FC_LIB_VARIANT / FC_HIPCC_FLAGS (tools only)   */
+uint32_t fc_build_flags(void);
 
 #ifdef __cplusplus
 }

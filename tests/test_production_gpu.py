@@ -1,0 +1,114 @@
+"""The k > 2 kernels at production shape.
+
+* C3 (BASELINE config 3: sec11 lattice, k = 4 quadrant plan, pair proposals, population
+  tolerance 0.05, base mu, 8192 chains per GPU, the multi-flip commit on by default): the lean
+  instance the bench times, 8192 chains in one launch, against the C oracle on 64 chains sampled
+  over the whole id range (final state, populations, every counter); the same chains split over
+  two ``chain_id_offset`` runs (two ranks' shards) are state-identical to the one run; and a
+  traced run of the same launch shape compared with the oracle proposal by proposal.
+* Long launches with the multi-flip commit on and off (C4 and C5 graphs, base-1 chains among
+  them, three 100,000-step launches): byte-identical checkpoints -- assignment, foreign-district
+  counts and their histogram, district tables, every per-chain scalar.
+"""
+import numpy as np
+import pytest
+
+from flipcomplexityempirical_amd import _lib
+from flipcomplexityempirical_amd import graphs as G
+from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+
+pytestmark = pytest.mark.gpu
+
+STAT_KEYS = ["steps", "proposals", "draws", "accepted", "inv_contig", "inv_pop", "sum_cut", "sum_nb",
+             "sum_wait", "sum_cut2", "sum_nb2", "wait_cur", "cut", "nb"]
+C3_SEED = 0x5EED0003  # bench.py's C3 seed
+
+
+def _c3(sec11, chains, *, offset=0, trace=0):
+    k = 4
+    a0 = sec11.assignment_array(G.quadrant_plan(sec11.nodes), list(range(k)))
+    _, (lo, hi) = G.population_bounds(sec11.n, k, 0.05)
+    cfg = RunConfig(k=k, labels=tuple(range(k)), proposal=_lib.FC_PROPOSE_PAIR, seed=C3_SEED, pop_lo=lo, pop_hi=hi,
+                    chain_id_offset=offset, trace_chains=trace, trace_cap=200000 if trace else 0)
+    run = FlipRun(FlipGraph(sec11), np.broadcast_to(a0, (chains, sec11.n)), cfg,
+                  bases=np.full(chains, G.SEC11_MU))
+    return run, a0, (lo, hi)
+
+
+def test_c3_production_shape_against_oracle(gpu, cref, sec11):
+    C, steps = 8192, 400
+    run, a0, (lo, hi) = _c3(sec11, C)
+    run.steps(steps)
+    name = run.kernel_name()
+    assert name.startswith("fc::flip_kernel<8,") and ", 3, false, true>" in name, name  # lean, multi-flip
+    st, state, pops = run.stats(), run.state(), run.pops()
+    assert (st["steps"] == steps).all() and not st["stuck"].any()
+    sample = np.unique(np.linspace(0, C - 1, 64).astype(np.int64))
+    for g in sample:
+        ref = cref.run(sec11, a0, base=G.SEC11_MU, pop_lo=lo, pop_hi=hi, seed=C3_SEED, chain_id=int(g),
+                       n_steps=steps, k=4, labels=[0, 1, 2, 3], log1mp=G.log1mp_table(sec11.n, 4), proposal=1)
+        assert np.array_equal(state[g], ref["final"]), g
+        for key in ("steps", "proposals", "draws", "accepted", "inv_contig", "inv_pop", "sum_cut", "sum_nb",
+                    "sum_wait", "cut", "nb"):
+            assert int(st[key][g]) == int(ref["stats"][key]), (g, key)
+        _, _, p_ref = G.cut_and_boundary(sec11, ref["final"])
+        assert np.array_equal(pops[g], p_ref), g
+    # two shards (two ranks' chain_id_offset) reproduce the one run chain for chain
+    for off, cnt in ((0, C // 2), (C // 2, C // 2)):
+        part, _, _ = _c3(sec11, cnt, offset=off)
+        part.steps(steps // 2)
+        part.steps(steps - steps // 2)
+        ps = part.stats()
+        assert np.array_equal(part.state(), state[off:off + cnt])
+        for key in STAT_KEYS:
+            assert np.array_equal(ps[key], st[key][off:off + cnt]), key
+        part.close()
+    run.close()
+
+
+def test_c3_production_launch_traced(gpu, cref, sec11):
+    """8192 chains per launch (the production grid), the first 64 traced per proposal."""
+    C, steps, T = 8192, 300, 64
+    run, a0, (lo, hi) = _c3(sec11, C, trace=T)
+    run.steps(steps)
+    for c in range(T):
+        ref = cref.run(sec11, a0, base=G.SEC11_MU, pop_lo=lo, pop_hi=hi, seed=C3_SEED, chain_id=c, n_steps=steps,
+                       k=4, labels=[0, 1, 2, 3], log1mp=G.log1mp_table(sec11.n, 4), trace_cap=200000, proposal=1)
+        tr, rt = run.trace(c), ref["trace"]
+        assert len(tr) == len(rt), c
+        for f in ("draw", "v", "flags", "cut", "nb", "wait"):
+            assert np.array_equal(tr[f], rt[f]), (c, f)
+    run.close()
+
+
+@pytest.mark.parametrize("case", ["c4", "c5"])
+def test_multi_flip_long_launches_checkpoint_identical(gpu, case):
+    """three 100,000-step launches of a few chains (base 1 among them, where most
+    passes commit several flips) with the multi-flip commit on and off leave byte-identical
+    checkpoints."""
+    if case == "c4":
+        spec, k = G.triangular_graph(100, 198), 8
+        a0 = spec.assignment_array(G.strip_plan(spec, k), list(range(k)))
+    else:
+        spec, k = G.delaunay_graph(10000, seed=0), 18
+        a0 = spec.assignment_array(G.bisection_plan(spec, k), list(range(k)))
+    fg = FlipGraph(spec)
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, 0.1)
+    inits = np.stack([a0] * 8)
+    bases = np.asarray([1.0, 0.5, 2.0, 1.0] * 2)
+    blobs, names = [], []
+    for mf in (1, -1):
+        cfg = RunConfig(k=k, labels=tuple(range(k)), proposal=_lib.FC_PROPOSE_PAIR, seed=77, pop_lo=lo, pop_hi=hi,
+                        tune={"multi_flip": mf})
+        r = FlipRun(fg, inits, cfg, bases=bases)
+        for _ in range(3):
+            r.steps(100000)
+        names.append(r.kernel_name())
+        assert (r.stats()["steps"] == 300000).all()
+        blobs.append(r.checkpoint())
+        r.close()
+    assert names[0].endswith(", true>") and names[1].endswith(", false>"), names
+    assert len(blobs[0]) == len(blobs[1])
+    a, b = np.frombuffer(blobs[0], np.uint8), np.frombuffer(blobs[1], np.uint8)
+    diff = np.nonzero(a != b)[0]
+    assert diff.size == 0, f"checkpoints differ at {diff.size} bytes, first at {diff[:4]}"

@@ -8,6 +8,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flipcomplexityempirical_amd import _lib  # noqa: E402
+_lib.load(allow_variant=True)  # A/B and profiling tool: FC_LIB_PATH / FC_LIB_VARIANT libraries allowed
 from flipcomplexityempirical_amd import graphs as G  # noqa: E402
 from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig  # noqa: E402
 

@@ -3,6 +3,7 @@ import sys, time, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 from flipcomplexityempirical_amd import graphs as G, _lib
+_lib.load(allow_variant=True)  # A/B and profiling tool: FC_LIB_PATH / FC_LIB_VARIANT libraries allowed
 from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune
 spec = G.sec11_graph(); fg = FlipGraph(spec)
 C = int(sys.argv[1]) if len(sys.argv) > 1 else 4096

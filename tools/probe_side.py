@@ -8,6 +8,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import bench
 from flipcomplexityempirical_amd import graphs as G
+from flipcomplexityempirical_amd import _lib  # noqa: E402
+_lib.load(allow_variant=True)  # A/B and profiling tool: FC_LIB_PATH / FC_LIB_VARIANT libraries allowed
 from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune
 
 W = bench.Workload(sys.argv[1])
