@@ -78,6 +78,38 @@ def lds_mix_peak_gbs(rmix: dict, wmix: dict, acc_per_prop: float) -> float:
 
 R_MIX, W_MIX = r_mix(4, 4), w_mix(4)
 R_BYTES, W_BYTES = sum(R_MIX.values()), sum(W_MIX.values())   # 59, 33
+L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate (4 MiB per XCD)
+
+
+def r_split(deg: float, ring_extra: float, extra4: float = 0.0):
+    """SURVEY §8(d)'s R split by where the bytes live on this implementation: the LDS-resident
+    chain state (boundary entry, a[v], a[] of the neighbours and ring cells, the district
+    populations; by access width) and the global node records every chain shares through L1 / L2
+    (row_ptr pair, col_idx and ring indices: NodeRec, fc_device.h)."""
+    lds = {2: 2.0, 1: 1.0 + deg + ring_extra, 4: 8.0 + extra4}
+    glob = 8.0 + 4 * deg + 4 * ring_extra
+    return lds, glob
+
+
+def roofline_levels(W, props: float, acc: float, kernel_ms: float, traffic=None) -> dict:
+    """Per-level roofline of one launch: the LDS-resident bytes against the
+    LDS aggregate at their access-width mix, the global node-record bytes against the L2
+    aggregate, the measured HBM bytes against HBM; ``bound`` = the level with the largest
+    fraction."""
+    t = kernel_ms * 1e-3
+    acc_pp = acc / props if props else 0.0
+    lds_b = sum(W.lds_mix.values()) * props + W.W * acc
+    lds_peak = lds_mix_peak_gbs(W.lds_mix, W.wmix, acc_pp)
+    glob_b = W.glob_bytes * props
+    out = {"lds": {"bytes": lds_b, "achieved": lds_b / t / 1e9, "peak": lds_peak,
+                   "frac": lds_b / t / 1e9 / lds_peak,
+                   "per_proposal": W.lds_mix, "per_accept": W.W},
+           "l2": {"bytes": glob_b, "achieved": glob_b / t / 1e9, "peak": L2_PEAK_GBS,
+                  "frac": glob_b / t / 1e9 / L2_PEAK_GBS, "per_proposal": W.glob_bytes},
+           "hbm": {"bytes": traffic, "achieved": traffic / t / 1e9 if traffic else None, "peak": HBM_PEAK_GBS,
+                   "frac": traffic / t / 1e9 / HBM_PEAK_GBS if traffic else None}}
+    out["bound"] = max((k for k in ("lds", "l2", "hbm") if out[k]["frac"] is not None), key=lambda k: out[k]["frac"])
+    return out
 
 
 class Workload:
@@ -142,6 +174,8 @@ class Workload:
                          % self.spec.n_edges)
         else:
             raise ValueError(f"unknown workload {name}")
+        self.lds_mix, self.glob_bytes = {"c2": r_split(4, 4), "c3": r_split(4, 4, extra4=8), "c4": r_split(6, 0)}.get(
+            name) or r_split(float(self.spec.degree().mean()), 0)
         self.seed = SEED + {"c2": 0, "c3": 1, "c4": 2, "c5": 3}[name]
         self.R, self.W = sum(self.rmix.values()), sum(self.wmix.values())
         if name != "c2":  # one configuration per base
@@ -180,6 +214,58 @@ def resident_chains(fg, W, device: int = 0) -> int:
     cus = torch.cuda.get_device_properties(device).multi_processor_count if torch.cuda.is_available() else 256
     lds = -(-lds // LDS_GRANULE) * LDS_GRANULE
     return cus * max(1, min(160 * 1024 // lds, 16))
+
+
+def measured_l2(wname: str, kname: str, chains: int, chain_steps: int, kernel_ms: float):
+    """The newest committed L1 / L2 counter summary of this workload's kernel at this launch shape
+    (profiles/*_<workload>_l1l2.json, tools/gpu_cache_pmc.sh), rescaled to this run's launch time:
+    L2 requests per launch priced at a 128-B line (an upper bound), hit rates, wave-state shares."""
+    import glob as _glob
+    best = None
+    for fn in sorted(_glob.glob(os.path.join(ROOT, "profiles", f"*_{wname}_l1l2.json"))):
+        try:
+            j = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        if j.get("kernel") == kname and j.get("chains") == chains and j.get("chain_steps") == chain_steps:
+            best = (fn, j)
+    if best is None:
+        return None
+    fn, j = best
+    m = j["measured"]
+    b = m.get("l2_bytes_upper")
+    return {"profile": os.path.relpath(fn, ROOT), "l2_bytes_upper_per_launch": b,
+            "l2_frac_upper": b / (kernel_ms * 1e-3) / 1e9 / L2_PEAK_GBS if b else None,
+            "tcc_hit_rate": m.get("tcc_hit_rate"), "l1_hit_rate_est": m.get("l1_hit_rate_est"),
+            "wait_any_frac": m.get("wait_any_frac"), "active_inst_any_frac": m.get("active_inst_any_frac")}
+
+
+def sweep_leg(replicas: int, device: int) -> dict:
+    """Side line: the reference's experiment as it is run (grid_chain_sec11.py:182-528,
+    Frankenstein_chain.py:182-556) -- both sweeps, 174 configurations x ``replicas`` chains of
+    100,000 yields, one launch per graph, every configuration's output set written (wait.txt, the
+    heatmap arrays, cut_times, the per-yield rce / rbn / slope / angle lists) into a scratch
+    directory that is removed afterwards.  Wall time from construction to the last file."""
+    import shutil
+    import tempfile
+    from flipcomplexityempirical_amd import sweep as SW
+    tmp = tempfile.mkdtemp(prefix="fc_sweep_")
+    try:
+        t0 = time.perf_counter()
+        res = SW.run_reference_sweeps(tmp, replicas=replicas, device=device)
+        wall = time.perf_counter() - t0
+        nbytes = sum(os.path.getsize(os.path.join(dp, f)) for dp, _, fs in os.walk(tmp) for f in fs)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    cfgs = sum(len(SW.sweep_configs(g)) for g in res)
+    return {"configurations": cfgs, "replicas": replicas, "yields_per_chain": 100000, "wall_s": wall,
+            "files": sum(r["files"] for r in res.values()), "bytes_written": nbytes,
+            "per_graph": {g: {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r["timing"].items()}
+                          for g, r in res.items()},
+            "note": "flipcomplexityempirical_amd.sweep.run_reference_sweeps: one fc_run per graph (per-chain bases "
+                    "and population bounds), full diagnostics + event log + corrected tallies, every "
+                    "configuration's files written by ChainResult.write_outputs (the reference runs the 174 "
+                    "configurations one after another on one CPU thread)"}
 
 
 def _free_port() -> int:
@@ -389,6 +475,9 @@ def main():
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sweep-replicas", type=int, default=1,
+                    help="side line (N = 1, c2): the reference's two sweeps -- all 174 configurations x R replicas, "
+                         "100,000 yields each, every output file written (flipcomplexityempirical_amd.sweep); 0: skip")
     ap.add_argument("--full-diag-steps", type=int, default=3,
                     help="launches of the full-diagnostics side line (0: skip)")
     ap.add_argument("--acf-yields", type=int, default=10 * 65536,
@@ -709,6 +798,8 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    levels = roofline_levels(W, per_launch_props, per_launch_acc, kernel_ms, traffic)
+    l1l2 = measured_l2(args.workload, kname, C, args.chain_steps, kernel_ms)
     out = {
         "metric": METRIC if args.workload == "c2" else f"flip proposals/sec, side workload {args.workload}",
         "value": value, "unit": "proposals/s", "n_gpus": world, "steps": args.steps,
@@ -729,13 +820,24 @@ def main():
         "accept_per_proposal": acc / props if props else None,
         "draws_per_proposal": float(agg[:, D.AGG_FIELDS.index("draws")].sum()) / props if props else None,
         "bfs_per_proposal": float((s1["bfs_calls"] - s0["bfs_calls"]).sum()) * world / props if props else None,
-        "roofline": {"bound": "lds", "achieved": achieved, "peak": lds_peak, "unit": "GB/s",
-                     "frac": achieved / lds_peak, "traffic": traffic,
-                     "peak_note": "LDS aggregate at the per-width rates of the algorithmic byte mix (MI355X_MICROARCH.md "
-                                  "§LDS: u8 / u16 / b32 reads 32 / 64 / 128 B/clk/CU, writes half; 256 CUs, 2.4 GHz; "
-                                  "reads %s B, writes %s B per accept, %.3f accepts per proposal)"
-                                  % (W.rmix, W.wmix, acc_pp),
-                     "peak_b128": LDS_PEAK_B128_GBS, "frac_b128": achieved / LDS_PEAK_B128_GBS,
+        "roofline": {"bound": levels["bound"], "achieved": levels[levels["bound"]]["achieved"],
+                     "peak": levels[levels["bound"]]["peak"], "unit": "GB/s",
+                     "frac": levels[levels["bound"]]["frac"], "traffic": traffic,
+                     "levels": levels,
+                     "levels_note": "SURVEY §8(d)'s algorithmic bytes split by where they live (bench.roofline_levels): "
+                                    "lds = the LDS-resident chain state (per proposal %s B by access width, every "
+                                    "write) against the LDS aggregate at that mix; l2 = the global node records "
+                                    "(row_ptr pair, col_idx, ring indices: %.0f B per proposal) against the L2 "
+                                    "aggregate (MI355X_MICROARCH.md §L2); hbm = measured bytes; bound = the largest "
+                                    "fraction; achieved / peak / frac above are the bound level's"
+                                    % (W.lds_mix, W.glob_bytes),
+                     "l2_measured": l1l2,
+                     "all_bytes_vs_lds": {"achieved": achieved, "peak": lds_peak, "frac": achieved / lds_peak,
+                                          "peak_b128": LDS_PEAK_B128_GBS, "frac_b128": achieved / LDS_PEAK_B128_GBS},
+                     "peak_note": "all_bytes_vs_lds: every algorithmic byte priced at the LDS aggregate of the byte "
+                                  "mix (MI355X_MICROARCH.md §LDS: u8 / u16 / b32 reads 32 / 64 / 128 B/clk/CU, writes "
+                                  "half; 256 CUs, 2.4 GHz; reads %s B, writes %s B per accept, %.3f accepts per "
+                                  "proposal), the round-3 pricing" % (W.rmix, W.wmix, acc_pp),
                      "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE "
                                      "(profiles/pmc_traffic.json; gfx950 FETCH_SIZE doubled)",
                      "kernel": kname,
@@ -749,6 +851,8 @@ def main():
     }
     if full_out is not None:
         out["full_diagnostics"] = full_out
+    if world == 1 and args.workload == "c2" and args.sweep_replicas > 0:
+        out["reference_sweeps"] = sweep_leg(args.sweep_replicas, local_rank)
     if node_out is not None:
         out["node_stream"] = node_out
     if world == 1 and not args.no_cpu_baseline:

@@ -51,6 +51,7 @@ struct fc_run {
     uint64_t *d_sbits = nullptr;  // k = 2 band stream: per chain, the band S as a bitmap (words u64)
     int32_t *d_mcnt = nullptr, *d_ngk = nullptr;  // k > 2 district-graph rule tables
     bool dgraph = false;
+    int32_t mf_marks = 0;        // k > 2 multi-flip commit: 0 off, 1 hashed neighbour marks, 2 exact marks
     int32_t wmax = 1;
     fc_event *d_events = nullptr;
     int64_t ev_cap = 0;
@@ -387,10 +388,23 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
                           // rule), thresholds, [BFS scratch | district tables], slots, district
                           // populations, wait queue; the multi-flip commit's hashed marks (last)
                           // only when it is on, so an "off" run keeps its residency
-        r->chain_lds_bytes = (r->dgraph ? 1 : 2) * r->npad + (2 * R + 2) * 8 +
-                             (r->dgraph ? fc::dgraph_lds_bytes(k) + (p->tune_multi_flip != -1 ? fc::hb_bytes(R) : 0)
-                                        : fc::bfs_bytes(n)) +
-                             5 * 64 * 4 + fc::kMaxKGeneral * 4 + fc::kNfh * 4 + fc::kWaitQK * 16;
+    {
+        const int base_b = (r->dgraph ? 1 : 2) * r->npad + (2 * R + 2) * 8 +
+                           (r->dgraph ? fc::dgraph_lds_bytes(k) : fc::bfs_bytes(n)) + 5 * 64 * 4 +
+                           fc::kMaxKGeneral * 4 + fc::kNfh * 4 + fc::kWaitQK * 16;
+        // chains per CU the LDS holds (granule 1280 B per one-wave workgroup, measured: DESIGN.md
+        // §4), capped by the 16 waves the k > 2 instances' registers allow
+        auto per_cu = [](int b) { return std::min(16, 160 * 1024 / (((b + 15) / 16 * 16 + 1279) / 1280 * 1280)); };
+        const int mf = p->tune_multi_flip;
+        r->mf_marks = 0;
+        if (!recom && k > 2 && r->dgraph && mf != -1) {
+            // exact marks (a byte per node) when they cost no residency, else the hashed set
+            const bool fits = per_cu(base_b + r->npad) >= per_cu(base_b + fc::hb_bytes(R));
+            r->mf_marks = mf == 2 ? 1 : mf == 3 ? 2 : (fits ? 2 : 1);
+        }
+        if (!recom && k > 2)  // (k = 2 above)
+            r->chain_lds_bytes = base_b + (r->mf_marks == 2 ? r->npad : r->mf_marks == 1 ? fc::hb_bytes(R) : 0);
+    }
     // PAIR slot bound: fc_params.wmax > 0 fixes it; otherwise the canonical stream's bound is
     // the state's largest foreign-district count (kept on the device, r->wmax = 0)
     r->wmax = 1;
@@ -427,8 +441,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         if (t.par_min < 1) return fail(FC_ERR_ARG, "fc_run_create: tune_par_min must be >= 1");
         // k > 2 with the district-graph rule: commit several independent flips per pass (64 /
         // RMAX of them).  Auto (0) = on (C4 +32 %, C3 +3.5 %)
-        if (p->tune_multi_flip < -1 || p->tune_multi_flip > 1)
-            return fail(FC_ERR_ARG, "fc_run_create: tune_multi_flip must be 0 (auto), 1 (on) or -1 (off)");
+        if (p->tune_multi_flip < -1 || p->tune_multi_flip > 3)
+            return fail(FC_ERR_ARG, "fc_run_create: tune_multi_flip must be 0 (auto), 1 (on), -1 (off), 2 (on, hashed "
+                                    "marks) or 3 (on, exact marks)");
         t.multi = p->tune_multi_flip != -1;
         const int qmax = k == 2 ? fc::kWaitQ : fc::kWaitQK;
         t.wait_q = p->tune_wait_queue ? p->tune_wait_queue : qmax;
@@ -826,7 +841,7 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.nsub = r->tune.nsub;
     k.hit_stop = r->tune.hit_stop;
     k.par_min = r->tune.par_min;
-    k.multi_flip = r->tune.multi ? 1 : 0;
+    k.multi_flip = r->tune.multi ? r->mf_marks : 0;
     k.wait_q = r->tune.wait_q;
     k.wpb = r->tune.wpb;
     k.coop = r->tune.coop ? 1 : 0;

@@ -49,8 +49,11 @@ using namespace dev;
 // spill, which costs C4's LDS-limited launch 2 %)
 // MF (KM = 3): the multi-flip commit below, in an instance of its own so that runs without it
 // keep the smaller code
-template <int RMAX, int NSUB, int KM, bool FULL, bool MF>
-__global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams p) {
+#ifndef FC_K_WAVES8
+#define FC_K_WAVES8 4  // RMAX = 8 waves per SIMD the register budget is sized for
+#endif
+template <int RMAX, int NSUB, int KM, bool FULL, int MF>
+__global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -106,6 +109,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
     // RMAX = 16, which keeps C5's chain at 11 LDS granules; a collision only ends a group early)
     uint32_t *hb = (uint32_t *)(ngk + 32);
     constexpr int kHbMask = fc::hb_bytes(RMAX) * 8 - 1;
+    // MF = 2 (graphs small enough, fc_run_create): exact marks instead, one byte per node (bit g:
+    // the g-th candidate of a pass has the node as a neighbour)
+    uint8_t *const mk8 = (uint8_t *)(ngk + 32);
+    uint32_t *const mk32 = (uint32_t *)mk8;
     // cooperative search control words (coop implies no district tables: they start here)
     int32_t *ctl = (int32_t *)(q_run + kWaitQK);
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
@@ -148,7 +155,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             const int kk = p.k * p.k;
             for (int i = lane; i < kk; i += kWave) mcnt[i] = p.mcnt[(size_t)c * kk + i];
             if (lane < 32) ngk[lane] = p.ngk[(size_t)c * 32 + lane];
-            if (KM == 3 && MF && lane < fc::hb_bytes(RMAX) / 4) hb[lane] = 0u;
+            if (KM == 3 && MF == 1 && lane < fc::hb_bytes(RMAX) / 4) hb[lane] = 0u;
+            if (KM == 3 && MF == 2)
+                for (int i = lane; i < npad / 4; i += kWave) mk32[i] = 0u;
             wave_sync();
             // adj[X] bit Y: some face holds cells of X and Y; bit 31: X touches the outer face
             uint32_t m = 0;
@@ -532,7 +541,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
             // parallel (lane group g = the g-th flip), then the district tables and the nf histogram
             // take the flips one by one in slot order, and the first flip that changes an adjacency
             // bit or the slot bound is the last one applied -- exactly the one-flip-at-a-time chain.
-            if constexpr (KM == 3 && MF) {
+            if constexpr (KM == 3 && MF != 0) {
                 constexpr int kGrp = 64 / RMAX;  // flips per pass (one lane per ring cell)
                 const uint64_t CANDM = __ballot(valid && acc) & lane_range(f, end);
                 if (__popcll(CANDM) >= 2) {
@@ -544,75 +553,142 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                     int cutP = kWave;   // first proposal whose population verdict changed
                     int dA = 0, dT = 0; // this slot's district populations moved by the taken flips
                     const int gi = lane / RMAX, ge = lane % RMAX;
+                    // lane group g <- the g-th flip (slot order) of mask M: its data, and this lane's
+                    // ring cell of it
+                    int mg, vm, Am, Tm, um;
+                    uint32_t pkm, pk2m, pk3m, nbrm;
+#define FC_MAP_GROUPS(M, CNT)                                                                 \
+    do {                                                                                      \
+        mg = gi < (CNT) ? select_bit64((M), gi) : f;                                          \
+        pkm = (uint32_t)__shfl((int)pk, mg);                                                  \
+        pk2m = (uint32_t)__shfl((int)pk2, mg);                                                \
+        pk3m = (uint32_t)__shfl((int)pk3, mg);                                                \
+        vm = (int)(pkm & 0x7fffu);                                                            \
+        Am = (int)((pkm >> 15) & 63u);                                                        \
+        Tm = (int)((pkm >> 21) & 63u);                                                        \
+        nbrm = pk2m >> 16;                                                                    \
+        uint32_t selm_ = 0;                                                                   \
+        _Pragma("unroll") for (int k2 = 0; k2 < RMAX / 2; ++k2) {                             \
+            const uint32_t w_ = (uint32_t)__shfl((int)rec.ring[k2], mg);                      \
+            if ((ge >> 1) == k2) selm_ = w_;                                                  \
+        }                                                                                     \
+        um = (int)((selm_ >> (16 * (ge & 1))) & 0xffffu);                                     \
+    } while (0)
+                    int nT = kGrp;  // MF = 2: the first candidate sharing a neighbour with an earlier one
+                    bool nb_k = false;  // MF = 2: this lane's cell is a neighbour of its group's candidate
+                    NodeRec<RMAX> ru;   // MF = 2: that neighbour's node record, loaded during the selection
+                    if constexpr (MF == 2) {
+                        // the first kGrp candidates mapped before the selection: their neighbours'
+                        // exact marks, all at once (byte u holds the candidates, bit g, having u as a
+                        // neighbour: one LDS round trip instead of one per member), and the
+                        // neighbours' records for the recount below, whose loads fly meanwhile
+                        const int nK = min(__popcll(CANDM), kGrp);
+                        FC_MAP_GROUPS(CANDM, nK);
+                        nb_k = gi < nK && ((nbrm >> ge) & 1u);
+                        ru = G[nb_k ? um : vm];
+                        if (nb_k) atomicOr(&mk32[um >> 2], (1u << gi) << (8 * (um & 3)));
+                        compiler_fence();
+                        const uint32_t mkv = nb_k ? (uint32_t)mk8[um] : 0u;
+                        const uint64_t CL = __ballot((mkv & ((1u << gi) - 1u)) != 0u);
+                        nT = CL ? (int)(__builtin_ctzll(CL) / RMAX) : nK;
+                    }
                     uint64_t CC = CANDM;
-                    for (; CC && nF < kGrp; CC &= CC - 1ull) {
+                    for (; CC && nF < nT; CC &= CC - 1ull) {
                         const int i = __builtin_ctzll(CC);
                         if (i >= cutA || i >= cutP) {
                             FC_PROF(i >= cutA ? 29 : 30, 1);
                             break;
                         }
-                        const int vi = rl32(v, i);
-                        const uint32_t pki = rlu(pk, i), nbri = rlu(pk2, i) >> 16;
-                        const int Ai = (int)((pki >> 15) & 63u), Ti = (int)((pki >> 21) & 63u);
-                        const int pvi = rl32(pv, i);
-                        uint32_t rwi[RMAX / 2];
+                        if constexpr (MF == 1) {  // (statement order kept: hipcc spills 13 more VGPRs otherwise)
+                            const int vi = rl32(v, i);
+                            const uint32_t pki = rlu(pk, i), nbri = rlu(pk2, i) >> 16;
+                            const int Ai = (int)((pki >> 15) & 63u), Ti = (int)((pki >> 21) & 63u);
+                            const int pvi = rl32(pv, i);
+                            uint32_t rwi[RMAX / 2];
 #pragma unroll
-                        for (int k2 = 0; k2 < RMAX / 2; ++k2) rwi[k2] = rlu(rec.ring[k2], i);
-                        // its neighbours against the marks of the flips taken before it
-                        uint32_t sel = rwi[0];
+                            for (int k2 = 0; k2 < RMAX / 2; ++k2) rwi[k2] = rlu(rec.ring[k2], i);
+                            // its neighbours against the marks of the flips taken before it
+                            uint32_t sel = rwi[0];
 #pragma unroll
-                        for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((ge >> 1) == k2) ? rwi[k2] : sel;
-                        const int ui = (int)((sel >> (16 * (ge & 1))) & 0xffffu);
-                        const bool isn = gi == 0 && ((nbri >> ge) & 1u);
-                        if (nF > 0) {
-                            const bool clash = isn && ((hb[(ui & kHbMask) >> 5] >> (ui & 31)) & 1u);
-                            if (__any(clash)) {
-                                FC_PROF(31, 1);
-                                break;
+                            for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((ge >> 1) == k2) ? rwi[k2] : sel;
+                            const int ui = (int)((sel >> (16 * (ge & 1))) & 0xffffu);
+                            const bool isn = gi == 0 && ((nbri >> ge) & 1u);
+                            if (nF > 0) {
+                                const bool clash = isn && ((hb[(ui & kHbMask) >> 5] >> (ui & 31)) & 1u);
+                                if (__any(clash)) {
+                                    FC_PROF(31, 1);
+                                    break;
+                                }
                             }
-                        }
-                        if (isn) atomicOr(&hb[(ui & kHbMask) >> 5], 1u << (ui & 31));
-                        FM |= 1ull << i;
-                        ++nF;
-                        // later slots whose node is vi or has vi in its own ring (rings are symmetric)
-                        bool stl = v == vi;
+                            if (isn) atomicOr(&hb[(ui & kHbMask) >> 5], 1u << (ui & 31));
+                            FM |= 1ull << i;
+                            ++nF;
+                            // later slots whose node is vi or has vi in its own ring (rings are symmetric)
+                            bool stl = v == vi;
 #pragma unroll
-                        for (int k2 = 0; k2 < RMAX / 2; ++k2)
-                            stl |= (rec.ring[k2] & 0xffffu) == (uint32_t)vi || (rec.ring[k2] >> 16) == (uint32_t)vi;
-                        const uint64_t SM = __ballot(stl && has && lane > i && lane < end);
-                        if (SM && __builtin_ctzll(SM) < cutA) cutA = __builtin_ctzll(SM);
-                        // the populations of later slots' districts after this flip
-                        dA += (av == Ti ? pvi : 0) - (av == Ai ? pvi : 0);
-                        dT += (tgt == Ti ? pvi : 0) - (tgt == Ai ? pvi : 0);
-                        const bool pok2 = (pa + dA - pv >= pop_lo) && (pb + dT + pv <= pop_hi);
-                        const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
-                        if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
+                            for (int k2 = 0; k2 < RMAX / 2; ++k2)
+                                stl |= (rec.ring[k2] & 0xffffu) == (uint32_t)vi || (rec.ring[k2] >> 16) == (uint32_t)vi;
+                            const uint64_t SM = __ballot(stl && has && lane > i && lane < end);
+                            if (SM && __builtin_ctzll(SM) < cutA) cutA = __builtin_ctzll(SM);
+                            // the populations of later slots' districts after this flip
+                            dA += (av == Ti ? pvi : 0) - (av == Ai ? pvi : 0);
+                            dT += (tgt == Ti ? pvi : 0) - (tgt == Ai ? pvi : 0);
+                            const bool pok2 = (pa + dA - pv >= pop_lo) && (pb + dT + pv <= pop_hi);
+                            const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
+                            if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
+                        } else {
+                            const int vi = rl32(v, i);
+                            const uint32_t pki = rlu(pk, i);
+                            const int Ai = (int)((pki >> 15) & 63u), Ti = (int)((pki >> 21) & 63u);
+                            const int pvi = rl32(pv, i);
+                            FM |= 1ull << i;
+                            ++nF;
+                            // later slots whose node is vi or has vi in its own ring (rings are symmetric)
+                            bool stl = v == vi;
+#pragma unroll
+                            for (int k2 = 0; k2 < RMAX / 2; ++k2)
+                                stl |= (rec.ring[k2] & 0xffffu) == (uint32_t)vi || (rec.ring[k2] >> 16) == (uint32_t)vi;
+                            const uint64_t SM = __ballot(stl && has && lane > i && lane < end);
+                            if (SM && __builtin_ctzll(SM) < cutA) cutA = __builtin_ctzll(SM);
+                            // the populations of later slots' districts after this flip
+                            dA += (av == Ti ? pvi : 0) - (av == Ai ? pvi : 0);
+                            dT += (tgt == Ti ? pvi : 0) - (tgt == Ai ? pvi : 0);
+                            const bool pok2 = (pa + dA - pv >= pop_lo) && (pb + dT + pv <= pop_hi);
+                            const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
+                            if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
+                        }
                     }
+                    if (MF == 2 && CC && nF == nT && nT < kGrp) FC_PROF(31, 1);
                     if (CC && nF == kGrp) FC_PROF(28, 1);
                     FC_STAMP(t_m1);
                     FC_PROF(23, t_m1 - t_m0);
                     const int f_last = 63 - __builtin_clzll(FM);
                     const int nv = __popcll(VAL & lane_range(f, f_last + 1));
-                    // the flip taken g-th, its data, and this lane's ring cell of it
-                    const int mg = gi < nF ? select_bit64(FM, gi) : f;
-                    const uint32_t pkm = (uint32_t)__shfl((int)pk, mg), pk2m = (uint32_t)__shfl((int)pk2, mg),
-                                   pk3m = (uint32_t)__shfl((int)pk3, mg);
-                    const int vm = (int)(pkm & 0x7fffu), Am = (int)((pkm >> 15) & 63u), Tm = (int)((pkm >> 21) & 63u);
-                    const uint32_t nbrm = pk2m >> 16;
-                    uint32_t selm = 0;
+                    if constexpr (MF == 1) {  // the flips taken (mapped here: keeps the selection's registers)
+                        mg = gi < nF ? select_bit64(FM, gi) : f;
+                        pkm = (uint32_t)__shfl((int)pk, mg);
+                        pk2m = (uint32_t)__shfl((int)pk2, mg);
+                        pk3m = (uint32_t)__shfl((int)pk3, mg);
+                        vm = (int)(pkm & 0x7fffu);
+                        Am = (int)((pkm >> 15) & 63u);
+                        Tm = (int)((pkm >> 21) & 63u);
+                        nbrm = pk2m >> 16;
+                        uint32_t selm = 0;
 #pragma unroll
-                    for (int k2 = 0; k2 < RMAX / 2; ++k2) {
-                        const uint32_t w = (uint32_t)__shfl((int)rec.ring[k2], mg);
-                        if ((ge >> 1) == k2) selm = w;
+                        for (int k2 = 0; k2 < RMAX / 2; ++k2) {
+                            const uint32_t w = (uint32_t)__shfl((int)rec.ring[k2], mg);
+                            if ((ge >> 1) == k2) selm = w;
+                        }
+                        um = (int)((selm >> (16 * (ge & 1))) & 0xffffu);
                     }
-                    const int um = (int)((selm >> (16 * (ge & 1))) & 0xffffu);
+#undef FC_MAP_GROUPS
                     const bool in_g = gi < nF;
                     const bool nb_m = in_g && ((nbrm >> ge) & 1u);
                     // exact recount of the neighbour's foreign districts before / after its flip,
                     // reading the flipped node's district as Am / Tm (nothing is written yet)
                     int old_m = 0, nfn_m = 0, au_m = 0;
                     if (nb_m) {
-                        const NodeRec<RMAX> ru = G[um];
+                        if constexpr (MF == 1) ru = G[um];
                         au_m = dist(um);
                         const uint32_t nbu = (uint32_t)(ru.meta >> kMetaNbrShift) & 0xffffu;
                         uint32_t du = 0, du0 = 0;
@@ -651,7 +727,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                         FC_PROF(27, 1);
                         // not worth it, or the launch's last step / an entering draw lies inside:
                         // clear the marks and take f alone
-                        if (nb_m) hb[(um & kHbMask) >> 5] = 0u;
+                        if constexpr (MF == 1) {
+                            if (nb_m) hb[(um & kHbMask) >> 5] = 0u;
+                        } else {
+                            if (nb_k) mk8[um] = 0u;
+                        }
                         compiler_fence();
                     } else {
                         // district tables and nf histogram: all flips at once, decrements before
@@ -748,7 +828,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip_kernel(KParams 
                         // the flips applied: districts and counts, populations, marks cleared
                         const bool app = gi < nA_;
                         const int pvm = __shfl(pv, mg);
-                        if (nb_m) hb[(um & kHbMask) >> 5] = 0u;
+                        if constexpr (MF == 1) {
+                            if (nb_m) hb[(um & kHbMask) >> 5] = 0u;
+                        } else {
+                            if (nb_k) mk8[um] = 0u;
+                        }
                         if (app && ge == 0) {
                             pkb[vm] = (uint8_t)(Tm | ((nf_af < 7 ? nf_af : 7) << 5));
                             atomicSub(&popk[Am], pvm);
@@ -1294,15 +1378,17 @@ int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, siz
             (void)hipFuncSetAttribute((const void *)flip_kernel<R, S, K, F, M>,                         \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
         if (name)                                                                                       \
-            snprintf(name, name_cap, "fc::flip_kernel<%d, %d, %d, %s%s>", R, S, K, F ? "true" : "false", \
-                     M ? ", true" : "");                                                                \
+            snprintf(name, name_cap, "fc::flip_kernel<%d, %d, %d, %s, %d>", R, S, K, F ? "true" : "false", \
+                     (int)(M));                                                                         \
         hipLaunchKernelGGL((flip_kernel<R, S, K, F, M>), grid, block, lds, s, p);                       \
     } while (0)
     // the multi-flip instance: district-graph rule, when the run asks for it
+    // (1: hashed marks; 2: exact marks, when fc_run_create found room for a byte per node)
 #define FC_LAUNCH(R, S, K, F)                                                     \
     do {                                                                          \
-        if (K == 3 && p.multi_flip) FC_LAUNCHM(R, S, K, F, (K == 3));         \
-        else FC_LAUNCHM(R, S, K, F, false);                                        \
+        if (K == 3 && p.multi_flip == 2) FC_LAUNCHM(R, S, K, F, (K == 3 ? 2 : 0)); \
+        else if (K == 3 && p.multi_flip) FC_LAUNCHM(R, S, K, F, (K == 3 ? 1 : 0)); \
+        else FC_LAUNCHM(R, S, K, F, 0);                                            \
     } while (0)
 #define FC_FULL_SWITCH(R, S, K)                          \
     do {                                                 \

@@ -178,7 +178,9 @@ typedef struct fc_params {
     int32_t stream;
     int32_t tune_multi_flip;    /* k > 2 with the district-graph rule: commit several independent
                                    accepted flips per pass (0: auto = on; 1: on; -1: one at a
-                                   time).
+                                   time; 2: on with the hashed neighbour marks; 3: on with exact
+                                   marks, one LDS byte per node -- on (0 / 1) takes the exact marks
+                                   when they cost no residency, fc_run_kernel_name shows which).
                                    Scheduling only, like every tune_* field                    */
 } fc_params;
 

@@ -355,18 +355,20 @@ def test_multi_flip_commit_equals_one_at_a_time(gpu, cref, sec11, case):
     run = _run_pair(spec, inits, bases, k, steps=steps, pct=pct, chunks=2, tune={"multi_flip": 1})
     name = run.kernel_name()
     assert ", 3, " in name, name
-    assert name.endswith(", true, true>"), name  # FULL (traced), multi-flip
+    assert name.endswith((", true, 1>", ", true, 2>")), name  # FULL (traced), multi-flip (hashed / exact marks)
     _check(cref, spec, run, k, inits, bases, steps=steps, pct=pct)
     fg = FlipGraph(spec)
     _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
     outs = []
-    for tune in ({"multi_flip": 1}, {"multi_flip": -1}):
+    # on (auto marks), off, and both mark forms forced (2: hashed, 3: exact)
+    for tune in ({"multi_flip": 1}, {"multi_flip": -1}, {"multi_flip": 2}, {"multi_flip": 3}):
         cfg = RunConfig(k=k, labels=tuple(range(k)), proposal=_lib.FC_PROPOSE_PAIR, seed=21, pop_lo=lo, pop_hi=hi,
                         tune=tune)
         r = FlipRun(fg, inits, cfg, bases=bases)
         r.steps(steps // 2)
         r.steps(steps - steps // 2)
         outs.append((r.stats(), r.state()))
-    for key in STAT_KEYS + ["wait_cur"]:
-        assert np.array_equal(outs[0][0][key], outs[1][0][key]), key
-    assert np.array_equal(outs[0][1], outs[1][1])
+    for o in outs[1:]:
+        for key in STAT_KEYS + ["wait_cur"]:
+            assert np.array_equal(outs[0][0][key], o[0][key]), key
+        assert np.array_equal(outs[0][1], o[1])

@@ -40,7 +40,8 @@ def test_c3_production_shape_against_oracle(gpu, cref, sec11):
     run, a0, (lo, hi) = _c3(sec11, C)
     run.steps(steps)
     name = run.kernel_name()
-    assert name.startswith("fc::flip_kernel<8,") and ", 3, false, true>" in name, name  # lean, multi-flip
+    # lean, multi-flip with the exact marks (a byte per node costs C3 no residency)
+    assert name.startswith("fc::flip_kernel<8,") and name.endswith(", 3, false, 2>"), name
     st, state, pops = run.stats(), run.state(), run.pops()
     assert (st["steps"] == steps).all() and not st["stuck"].any()
     sample = np.unique(np.linspace(0, C - 1, 64).astype(np.int64))
@@ -81,19 +82,23 @@ def test_c3_production_launch_traced(gpu, cref, sec11):
     run.close()
 
 
-@pytest.mark.parametrize("case", ["c4", "c5"])
+@pytest.mark.parametrize("case", ["c3", "c4", "c5"])
 def test_multi_flip_long_launches_checkpoint_identical(gpu, case):
     """three 100,000-step launches of a few chains (base 1 among them, where most
     passes commit several flips) with the multi-flip commit on and off leave byte-identical
-    checkpoints."""
-    if case == "c4":
+    checkpoints (C3: the exact-mark instance; C4 / C5: the hashed one)."""
+    pct = 0.1
+    if case == "c3":
+        spec, k, pct = G.sec11_graph(), 4, 0.05
+        a0 = spec.assignment_array(G.quadrant_plan(spec.nodes), list(range(k)))
+    elif case == "c4":
         spec, k = G.triangular_graph(100, 198), 8
         a0 = spec.assignment_array(G.strip_plan(spec, k), list(range(k)))
     else:
         spec, k = G.delaunay_graph(10000, seed=0), 18
         a0 = spec.assignment_array(G.bisection_plan(spec, k), list(range(k)))
     fg = FlipGraph(spec)
-    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, 0.1)
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
     inits = np.stack([a0] * 8)
     bases = np.asarray([1.0, 0.5, 2.0, 1.0] * 2)
     blobs, names = [], []
@@ -107,7 +112,8 @@ def test_multi_flip_long_launches_checkpoint_identical(gpu, case):
         assert (r.stats()["steps"] == 300000).all()
         blobs.append(r.checkpoint())
         r.close()
-    assert names[0].endswith(", true>") and names[1].endswith(", false>"), names
+    # C4 / C5 keep the hashed marks (exact ones would cost them residency), off: MF = 0
+    assert names[0].endswith(", 2>" if case == "c3" else ", 1>") and names[1].endswith(", 0>"), names
     assert len(blobs[0]) == len(blobs[1])
     a, b = np.frombuffer(blobs[0], np.uint8), np.frombuffer(blobs[1], np.uint8)
     diff = np.nonzero(a != b)[0]
