@@ -577,12 +577,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                     int nT = kGrp;  // MF = 2: the first candidate sharing a neighbour with an earlier one
                     bool nb_k = false;  // MF = 2: this lane's cell is a neighbour of its group's candidate
                     NodeRec<RMAX> ru;   // MF = 2: that neighbour's node record, loaded during the selection
-                    const int nK = min(__popcll(CANDM), kGrp);  // (MF = 2) candidates considered
                     if constexpr (MF == 2) {
                         // the first kGrp candidates mapped before the selection: their neighbours'
                         // exact marks, all at once (byte u holds the candidates, bit g, having u as a
                         // neighbour: one LDS round trip instead of one per member), and the
                         // neighbours' records for the recount below, whose loads fly meanwhile
+                        const int nK = min(__popcll(CANDM), kGrp);
                         FC_MAP_GROUPS(CANDM, nK);
                         nb_k = gi < nK && ((nbrm >> ge) & 1u);
                         ru = G[nb_k ? um : vm];
@@ -592,14 +592,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                         const uint64_t CL = __ballot((mkv & ((1u << gi) - 1u)) != 0u);
                         nT = CL ? (int)(__builtin_ctzll(CL) / RMAX) : nK;
                     }
-                    if constexpr (MF == 1) {  // member by member (statement order kept: hipcc spills 13 more VGPRs otherwise)
-                        uint64_t CC = CANDM;
-                        for (; CC && nF < nT; CC &= CC - 1ull) {
-                            const int i = __builtin_ctzll(CC);
-                            if (i >= cutA || i >= cutP) {
-                                FC_PROF(i >= cutA ? 29 : 30, 1);
-                                break;
-                            }
+                    uint64_t CC = CANDM;
+                    for (; CC && nF < nT; CC &= CC - 1ull) {
+                        const int i = __builtin_ctzll(CC);
+                        if (i >= cutA || i >= cutP) {
+                            FC_PROF(i >= cutA ? 29 : 30, 1);
+                            break;
+                        }
+                        if constexpr (MF == 1) {  // (statement order kept: hipcc spills 13 more VGPRs otherwise)
                             const int vi = rl32(v, i);
                             const uint32_t pki = rlu(pk, i), nbri = rlu(pk2, i) >> 16;
                             const int Ai = (int)((pki >> 15) & 63u), Ti = (int)((pki >> 21) & 63u);
@@ -636,58 +636,30 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                             const bool pok2 = (pa + dA - pv >= pop_lo) && (pb + dT + pv <= pop_hi);
                             const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
                             if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
-                        }
-                        if (CC && nF == kGrp) FC_PROF(28, 1);
-                    } else {
-                        // every slot against every candidate at once (registers only, no ballot per
-                        // member): a_s = the first candidate (rank) before this slot whose node is in
-                        // its view, b_s = the first one after whose flip (with those before it) this
-                        // proposal's population verdict changes.  Candidate t is taken iff no slot s at
-                        // or before it has min(a_s, b_s) < t, no earlier candidate shares a neighbour
-                        // with it (nT), t < kGrp: the member-by-member selection, all at once
-                        int a_s = kGrp, b_s = kGrp;
-#pragma unroll
-                        for (int g = 0; g < kGrp; ++g) {
-                            if (g >= nK) break;
-                            const int ig = rl32(mg, g * RMAX);
-                            const uint32_t pkg = rlu(pkm, g * RMAX);
-                            const int vg = (int)(pkg & 0x7fffu), Ag = (int)((pkg >> 15) & 63u), Tg = (int)((pkg >> 21) & 63u);
-                            const int pvg = rl32(pv, ig);
-                            bool stl = v == vg;
+                        } else {
+                            const int vi = rl32(v, i);
+                            const uint32_t pki = rlu(pk, i);
+                            const int Ai = (int)((pki >> 15) & 63u), Ti = (int)((pki >> 21) & 63u);
+                            const int pvi = rl32(pv, i);
+                            FM |= 1ull << i;
+                            ++nF;
+                            // later slots whose node is vi or has vi in its own ring (rings are symmetric)
+                            bool stl = v == vi;
 #pragma unroll
                             for (int k2 = 0; k2 < RMAX / 2; ++k2)
-                                stl |= (rec.ring[k2] & 0xffffu) == (uint32_t)vg || (rec.ring[k2] >> 16) == (uint32_t)vg;
-                            const bool after = lane > ig;
-                            if (a_s == kGrp && stl && after && has && lane < end) a_s = g;
-                            dA += (av == Tg ? pvg : 0) - (av == Ag ? pvg : 0);
-                            dT += (tgt == Tg ? pvg : 0) - (tgt == Ag ? pvg : 0);
+                                stl |= (rec.ring[k2] & 0xffffu) == (uint32_t)vi || (rec.ring[k2] >> 16) == (uint32_t)vi;
+                            const uint64_t SM = __ballot(stl && has && lane > i && lane < end);
+                            if (SM && __builtin_ctzll(SM) < cutA) cutA = __builtin_ctzll(SM);
+                            // the populations of later slots' districts after this flip
+                            dA += (av == Ti ? pvi : 0) - (av == Ai ? pvi : 0);
+                            dT += (tgt == Ti ? pvi : 0) - (tgt == Ai ? pvi : 0);
                             const bool pok2 = (pa + dA - pv >= pop_lo) && (pb + dT + pv <= pop_hi);
-                            if (b_s == kGrp && prop && after && pok2 != popok) b_s = g;
+                            const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
+                            if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
                         }
-                        const int c_s = min(a_s, b_s);
-                        // the first candidate this slot blocks: rank max(c_s + 1, candidates below it)
-                        const int tb = c_s < kGrp ? max(c_s + 1, __popcll(CANDM & bits_below(lane))) : kGrp;
-                        int T = kGrp;  // smallest tb over the wave (binary search over 1..kGrp)
-                        {
-                            int lo = 1, hi = kGrp;
-                            if (__ballot(tb < kGrp)) {
-                                hi = kGrp - 1;
-                                while (lo < hi) {
-                                    const int mid = (lo + hi) >> 1;
-                                    if (__ballot(tb <= mid)) hi = mid;
-                                    else lo = mid + 1;
-                                }
-                                T = lo;
-                            }
-                        }
-                        nF = min(min(T, nT), nK);
-                        FM = CANDM & bits_below(select_bit64(CANDM, nF - 1) + 1);
-                        const uint64_t SA = __ballot(a_s < nF);
-                        if (SA) cutA = __builtin_ctzll(SA);
-                        if (nF == nT && nT < nK) FC_PROF(31, 1);
-                        else if (nF == T && T < nK) FC_PROF(__ballot(tb == T && a_s < b_s) ? 29 : 30, 1);
-                        else if (nF == kGrp && __popcll(CANDM) > kGrp) FC_PROF(28, 1);
                     }
+                    if (MF == 2 && CC && nF == nT && nT < kGrp) FC_PROF(31, 1);
+                    if (CC && nF == kGrp) FC_PROF(28, 1);
                     FC_STAMP(t_m1);
                     FC_PROF(23, t_m1 - t_m0);
                     const int f_last = 63 - __builtin_clzll(FM);
