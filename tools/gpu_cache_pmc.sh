@@ -9,7 +9,7 @@ TAG=$1; shift
 for w in "${@:-c2}"; do
   OUT=$R/gpurun_out/cache_${TAG}_$w; mkdir -p "$OUT"
   if [ $w = c2 ]; then
-    B="bench.py --steps 2 --warmup 1 --no-cpu-baseline --full-diag-steps 0"
+    B="bench.py --steps 2 --warmup 1 --no-cpu-baseline --full-diag-steps 0 --sweep-replicas 0"
   else
     B="bench.py --workload $w --steps 2 --warmup 1 --chain-steps 20000 --no-cpu-baseline --full-diag-steps 0"
   fi

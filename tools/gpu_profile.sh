@@ -7,12 +7,12 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 TAG=${1:-r02}
 OUT=$R/gpurun_out/prof_$TAG; mkdir -p "$OUT"
-BENCH="bench.py --steps 5 --warmup 1 --no-cpu-baseline --full-diag-steps 0"
+BENCH="bench.py --steps 5 --warmup 1 --no-cpu-baseline --full-diag-steps 0 --sweep-replicas 0"
 timeout -k 10 600 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail -20 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $BENCH > "$OUT/trace.log" 2>&1 || { echo "trace failed"; tail -20 "$OUT/trace.log"; exit 1; }
 # the full-diagnostics leg (the reference loop body's tallies) in its own traced run
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_full" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --full-diag-steps 3 > "$OUT/trace_full.log" 2>&1 || { echo "trace full failed"; tail -20 "$OUT/trace_full.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_full" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --full-diag-steps 3 --sweep-replicas 0 > "$OUT/trace_full.log" 2>&1 || { echo "trace full failed"; tail -20 "$OUT/trace_full.log"; exit 1; }
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $C -d "$OUT/pmc_$C" -o pmc --output-format csv -- python3 $BENCH > "$OUT/pmc_$C.log" 2>&1 || { echo "pmc $C failed"; tail -20 "$OUT/pmc_$C.log"; exit 1; }
 done

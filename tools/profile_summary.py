@@ -40,12 +40,17 @@ if os.path.exists(os.path.join(src, "trace_full", "run_kernel_stats.csv")):  # f
     shutil.copy(os.path.join(src, "trace_full", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats_full.csv"))
 
 # per-launch durations of the headline kernel in the traced bench (steps 5, warmup 1)
+# (exactly the bench line's instance: other flip kernels of the run -- e.g. a reference-sweep side
+# line's full-diagnostics instance -- are not the headline's launches)
+KNAME = bench["roofline"]["kernel"]
 trace = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
-         if "fc::flip2_kernel" in r["Kernel_Name"]]
+         if KNAME + "(" in r["Kernel_Name"]]
 durs = [(float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) * 1e-6 for r in trace]
 timed = durs[1:]  # drop the warmup launch
 rl = bench["roofline"]
-alg = rl["alg_bytes_per_launch"]
+# the bound level's algorithmic bytes (roofline.levels, round 4) -- the bytes achieved is priced on
+lvl = rl.get("levels", {}).get(rl["bound"]) if isinstance(rl.get("levels"), dict) else None
+alg = lvl["bytes"] if lvl else rl["alg_bytes_per_launch"]
 check = {"round": tag, "kernel": trace[0]["Kernel_Name"] if trace else None,
          "rocprof_launch_ms": durs, "rocprof_timed_mean_ms": statistics.mean(timed),
          "rocprof_timed_median_ms": statistics.median(timed),
@@ -58,7 +63,7 @@ check["frac_from_rocprof"] = check["achieved_gbs_from_rocprof"] / rl["peak"]
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     rows = [r for r in flip_rows(os.path.join(src, f"pmc_{c}", "pmc_counter_collection.csv"))
-            if "fc::flip2_kernel" in r["Kernel_Name"]]
+            if KNAME + "(" in r["Kernel_Name"]]
     vals[c] = [float(r["Counter_Value"]) for r in rows][1:]  # timed launches
 fetch = statistics.mean(vals["FETCH_SIZE"])
 write = statistics.mean(vals["WRITE_SIZE"])
@@ -103,7 +108,7 @@ def lds_issue(path, kname):
                    "x 256 B/clk/CU bounds the LDS bytes moved from above"}
 
 
-lds = lds_issue(os.path.join(src, "pmc_lds", "pmc_counter_collection.csv"), "fc::flip2_kernel")
+lds = lds_issue(os.path.join(src, "pmc_lds", "pmc_counter_collection.csv"), KNAME + "(")
 json.dump(lds, open(os.path.join(dst, f"{tag}_lds_issue.json"), "w"), indent=1)
 check["lds_array_busy_frac"] = lds["lds_array_busy_frac"]
 json.dump(check, open(os.path.join(dst, f"{tag}_roofline_check.json"), "w"), indent=1)
