@@ -87,6 +87,7 @@ __device__ __forceinline__ int ring_entry(const uint32_t (&ring)[RMAX / 2], int 
 }
 
 using fc::one_run;  // fc_ring.h
+using fc::one_run_flat;
 
 // Chain dealing (fc_deal.hip): the chain this wave runs.  Lane 0 reads the wave's SIMD
 // (HW_ID: SIMD, pipe, CU, SH, SE; XCC_ID: the XCD), takes the next arrival slot s on that

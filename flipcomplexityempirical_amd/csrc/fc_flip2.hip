@@ -361,7 +361,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 vd = (int)(m >> 32);
                 okd = inrange && (uint32_t)m >= p.lemire_thresh;
             }
-            const bool hitd = okd && fcnt[vd] != 0;
+            // (vd < n for every lane: the read needs no guard, and a short-circuit && would put it
+            // behind an exec-mask branch)
+            const bool hitd = okd & (fcnt[vd] != 0);
             const uint64_t hm = __ballot(hitd);
             const int sp = nh + count_below(hm);
             if (hitd && sp < 64) {
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             } else {
                 gen = (uint64_t)(gen + 64) < room ? gen + 64 : (int)room;
             }
-            if (okd && !hitd && lane < used) rv[r] = vd | (sp << 16);
+            rv[r] = (okd & !hitd & (lane < used)) ? (vd | (sp << 16)) : rv[r];
             nh += cnt;
         }
         const int ns = nh < 64 ? nh : 64;
@@ -388,9 +390,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
 
         // ---- 2. every slot against the current state --------------------------------------
         const bool has = lane < ns;
-        int off_l = has ? (int)slot[192 + lane] : gen;
+        // (the slot array is always readable: unconditional reads and a select, no exec-mask branch)
+        const int off_r = (int)slot[192 + lane], v_r = (int)slot[lane];
+        int off_l = has ? off_r : gen;
         const uint64_t d = draw + (uint64_t)off_l;
-        int v = has ? (int)slot[lane] : 0;
+        int v = has ? v_r : 0;
         const uint32_t w1 = slot[64 + lane], w2 = slot[128 + lane];
         const NodeRec<RMAX> rec = G[v];
         int av = a[v];
@@ -400,13 +404,15 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         uint32_t nbr = (uint32_t)(rec.meta >> kMetaNbrShift) & 0xffffu;
         const uint32_t link = (uint32_t)(rec.meta >> kMetaLinkShift) & 0xffffu;
         int cell[RMAX];  // ring cells (padded with the node itself)
-        uint32_t inA = 0;
+        // districts are 0 / 1: pack the ring's district-1 bits, then A's bits are those or
+        // their complement (shift-ors, no compare / select per cell)
+        uint32_t in1 = 0;
 #pragma unroll
         for (int i = 0; i < RMAX; ++i) {
             cell[i] = ring_entry<RMAX>(rec.ring, i);
-            inA |= (uint32_t)(a[cell[i]] == av) << i;
+            in1 |= (uint32_t)a[cell[i]] << i;
         }
-        inA &= full;
+        uint32_t inA = (av ? in1 : ~in1) & full;
         slot[256 + lane] = link | (Ln << 16);  // for re-evaluations inside the commit
         // target district: 1 - av (-1 * assignment, grid_chain_sec11.py:145)
         const uint32_t nbrA = inA & nbr;        // old-district neighbours
@@ -418,9 +424,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         {
             const uint32_t rot = Ln ? (((inA >> 1) | (inA << (Ln - 1))) & full) : 0u;
             const uint32_t lk = inA & rot & link;
-            s_lin = one_run(nbrA, full & ~lk, full);
-            const uint32_t vlink = (Ln >= 2 && (inA & 1u) && ((inA >> (Ln - 1)) & 1u)) ? (1u << (Ln - 1)) : 0u;
-            s_cyc = one_run(nbrA, full & ~(lk | vlink), full);
+            s_lin = one_run_flat(nbrA, full & ~lk, full);
+            // the ring's closing step (cell Ln-1 to cell 0), when both ends are in A
+            const uint32_t vlink = (Ln >= 2) ? ((inA & (inA >> (Ln - 1)) & 1u) << (Ln - 1)) : 0u;
+            s_cyc = one_run_flat(nbrA, full & ~(lk | vlink), full);
         }
         const bool exact = SEARCH ? (rec.meta & kMetaExact) && !force_bfs : true;
         const bool gam = (rec.meta & kMetaGamma) != 0;
@@ -459,28 +466,21 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // (no ring reads; the threshold read issues beside the slot reads)
         auto reeval = [&](int from, int vfx, uint32_t eqx) {
             FC_STAMP(t_re0);
-            if (st & LF_WROTE) {
-                smark[v] = 0xff;
-#pragma unroll
-                for (int i = 0; i < RMAX; ++i) FC_ST(((nbr >> i) & 1u), nmark[cell[i]], 0xff);
-            }
-            st &= ~LF_WROTE;
+            // (no marks to clear: every segment pass clears its own before anything else runs)
             compiler_fence();
             if (has && lane >= from) {
                 const uint32_t lkl = slot[256 + lane];
                 const uint32_t w1r = slot[64 + lane], w2r = slot[128 + lane];
                 if (vfx < 0) {
                     av = a[v];
-                    uint32_t ia = 0;
+                    uint32_t i1 = 0;
 #pragma unroll
-                    for (int i = 0; i < RMAX; ++i) ia |= (uint32_t)(a[cell[i]] == av) << i;
-                    inA = ia;
+                    for (int i = 0; i < RMAX; ++i) i1 |= (uint32_t)a[cell[i]] << i;
+                    inA = av ? i1 : ~i1;
                 } else {
-                    if (v == vfx) {  // its own node flipped: every ring relation inverts
-                        av = 1 - av;
-                        inA = ~inA;
-                    }
-                    inA ^= eqx;
+                    const bool self = v == vfx;  // its own node flipped: every ring relation inverts
+                    av = self ? 1 - av : av;
+                    inA = (self ? ~inA : inA) ^ eqx;
                 }
                 // nbr has no bits at or above the ring length: these need no length mask
                 const uint32_t nbA = inA & nbr;
@@ -493,9 +493,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 inA &= fl;
                 const uint32_t rot = L2 ? (((inA >> 1) | (inA << (L2 - 1))) & fl) : 0u;
                 const uint32_t lk = inA & rot & lnk;
-                const bool sl = one_run(nbA, fl & ~lk, fl);
-                const uint32_t vlink = (L2 >= 2 && (inA & 1u) && ((inA >> (L2 - 1)) & 1u)) ? (1u << (L2 - 1)) : 0u;
-                const bool sc = one_run(nbA, fl & ~(lk | vlink), fl);
+                const bool sl = one_run_flat(nbA, fl & ~lk, fl);
+                const uint32_t vlink = (L2 >= 2) ? ((inA & (inA >> (L2 - 1)) & 1u) << (L2 - 1)) : 0u;
+                const bool sc = one_run_flat(nbA, fl & ~(lk | vlink), fl);
                 const bool ac = mant53(w1r, w2r) < th;
                 st = (st & (LF_EXACT | LF_GAM | LF_HAS | LF_FRZ)) | (tmask != 0u ? LF_HIT : 0u) | (ac ? LF_ACC : 0u) |
                      (sl ? LF_SLIN : 0u) | (sc ? LF_SCYC : 0u);
@@ -536,22 +536,24 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             // be hoisted as lane masks into SGPRs and spilled
             asm volatile("" : "+v"(st), "+v"(inA), "+v"(tmask), "+v"(nbr), "+v"(delta), "+v"(nA), "+v"(av), "+v"(pv),
                          "+v"(v), "+v"(off_l));
+            // (SEARCH = false: every node exact and no search verdicts -- compile-time constants,
+            // so the lean instance carries no undecided-slot logic)
             const bool hit = (st & LF_HIT) != 0, acc = (st & LF_ACC) != 0, s_lin = (st & LF_SLIN) != 0,
-                       s_cyc = (st & LF_SCYC) != 0, exact = (st & LF_EXACT) != 0, gam = (st & LF_GAM) != 0,
-                       has = (st & LF_HAS) != 0;
+                       s_cyc = (st & LF_SCYC) != 0, exact = SEARCH ? (st & LF_EXACT) != 0 : true,
+                       gam = (st & LF_GAM) != 0, has = (st & LF_HAS) != 0;
             const bool prop = hit & (lane >= pos) & (lane < end);
             // contiguity verdict when the other district does (okT) / does not (okN) touch
             // the outer face -- the outer-face counts are chain-global
             // (selects, not an if-chain: the chain compiled to nested exec-mask branches)
             // BFS verdict if any; no old-district neighbour: invalid; else the run rule, exact
             // or (not exact) deciding only "one run"
-            const bool bd = (st & ST_BD) != 0, br = (st & ST_BR) != 0, nz = nA != 0;
+            const bool bd = SEARCH && (st & ST_BD) != 0, br = SEARCH && (st & ST_BR) != 0, nz = nA != 0;
             const bool okT = bd ? br : (nz & s_lin);
             const bool okN = bd ? br : (nz & ((exact & gam) ? s_cyc : s_lin));
             const bool known = bd | !nz | exact | s_lin;
             const bool ok = ((av ? ng0 : ng1) > 0) ? okT : okN;
             const int pa = av ? pops1 : pops0, pb = av ? pops0 : pops1;
-            const bool popok = (pa - pv >= pop_lo) && (pb + pv <= pop_hi);
+            const bool popok = (pa - pv >= pop_lo) & (pb + pv <= pop_hi);
             bool valid = prop & known & ok & popok;
             bool acc_now = acc;
             bool inv_contig = !ok;  // reason of an invalid proposal: contiguity, else "pop"
@@ -613,7 +615,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 const int Gp = count_below(__ballot(cand0 && dg_l > 0)) - count_below(__ballot(cand0 && dg_l < 0));
                 const bool ok1 = ((av ? ng0 + Gp : ng1 - Gp) > 0) ? okT : okN;
                 const int q0 = pops0 + P, q1 = pops1 - P;
-                const bool valid1 = prop && known && ok1 && ((av ? q1 : q0) - pv >= pop_lo) &&
+                const bool valid1 = prop & known & ok1 & ((av ? q1 : q0) - pv >= pop_lo) &
                                     ((av ? q0 : q1) + pv <= pop_hi);
                 const bool cand1 = valid1 && acc;
                 const uint64_t MM = __ballot(prop && cand1 != cand0);
@@ -634,7 +636,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 bool stale_seg = false;
                 if (K) {
                     const bool inK = (K >> lane) & 1ull;
-                    if (inK) st |= LF_WROTE;
+                    st |= inK ? LF_WROTE : 0u;
                     // marks: smark[node] / nmark[neighbour] = lowest candidate lane (0xff: none).
                     // Every segment pass clears its marks (below), so the first round writes without
                     // reading.  Stores to one byte from later instructions win (a node is a
@@ -745,22 +747,21 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     for (int i = 0; i < RMAX; ++i) oldc[i] = fcnt[cell[i]];
                     compiler_fence();
                     int dnb = 0;
+                    // (bit masks, not short-circuit tests: those compiled to a branch per cell)
+                    const uint32_t nbm = me ? nbr : 0u, upm = inA & nbm, dnm = tmask & nbm;
 #pragma unroll
                     for (int i = 0; i < RMAX; ++i) {
-                        const bool nb_i = me && ((nbr >> i) & 1u);
-                        const uint32_t up = (inA >> i) & 1u, dn = (tmask >> i) & 1u;  // dlt = up - dn
-                        FC_ST(nb_i, fcnt[cell[i]], oldc[i] + (int)up - (int)dn);
-                        dnb += nb_i ? (int)(up & (uint32_t)(oldc[i] == 0)) - (int)(dn & (uint32_t)(oldc[i] == 1)) : 0;
+                        const uint32_t up = (upm >> i) & 1u, dn = (dnm >> i) & 1u;  // dlt = up - dn
+                        FC_ST((nbm >> i) & 1u, fcnt[cell[i]], oldc[i] + (int)up - (int)dn);
+                        dnb += (int)(up & (uint32_t)(oldc[i] == 0)) - (int)(dn & (uint32_t)(oldc[i] == 1));
                     }
                     FC_ST(me, *(uint8_t *)&a[v], 1 - av);
                     FC_ST(me, fcnt[v], nA);
                     const int pkd = me ? ((delta + 32) | ((dnb + 32) << 16)) : 0;
                     const int S = wave_scan_incl(pkd);
                     const int cntA = count_below(AP) + 1;
-                    if (me) {
-                        cut_after = cut + (S & 0xffff) - 32 * cntA;
-                        nb_after = nb + (S >> 16) - 32 * cntA;
-                    }
+                    cut_after = me ? cut + (S & 0xffff) - 32 * cntA : cut_after;
+                    nb_after = me ? nb + (S >> 16) - 32 * cntA : nb_after;
                     const int L = 63 - __builtin_clzll(AP);
                     cut = rl32(cut_after, L);
                     nb = rl32(nb_after, L);
@@ -772,10 +773,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     last_flip = rl32(v, L);
                     compiler_fence();
                 }
-                if (st & LF_WROTE) {  // clear this pass's marks: the next pass starts clean
+                // clear this pass's marks: the next pass (and the next batch) starts clean.  Every
+                // mark is 0xff between passes, so the lanes that wrote clear their whole ring
+                // (cells that are not neighbours hold 0xff already; padding cells are the node)
+                if (st & LF_WROTE) {
                     smark[v] = 0xff;
 #pragma unroll
-                    for (int i = 0; i < RMAX; ++i) FC_ST(((nbr >> i) & 1u), nmark[cell[i]], 0xff);
+                    for (int i = 0; i < RMAX; ++i) nmark[cell[i]] = 0xff;
                     st &= ~LF_WROTE;
                 }
                 FC_STAMP(t_sg1);
@@ -812,13 +816,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const uint32_t bits = valid ? ST_VS : (inv_contig ? ST_IC : ST_IP);
             if (nvalid >= rem) {  // the launch's last step lies before f
                 const int e = kth_set_bit(segv, rem);
-                if (prop && lane <= e) st |= bits;
+                st |= (prop & (lane <= e)) ? bits : 0u;
                 rem = 0;
                 end = e + 1;
                 target_hit = true;
                 break;
             }
-            if (prop && lane < f) st |= bits;
+            st |= (prop & (lane < f)) ? bits : 0u;
             rem -= nvalid;
             pos = f;
             if (f >= end) break;
@@ -844,14 +848,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const bool is_nbr = lane < RMAX && ((nbrf >> lane) & 1u);
             // foreign-neighbour counts: u sees v leave A (+1 if u in A) and join t (-1 if u in t)
             const int dlt = (int)((inAf >> lane) & 1u) - (int)((tmf >> lane) & 1u);
-            bool enter = false, leave = false, outS = false;
-            if (is_nbr) {
-                const int old = fcnt[my_e];
-                const uint64_t swd = BAND ? sb[my_e >> 6] : 0ull;
-                fcnt[my_e] = (uint8_t)(old + dlt);
-                enter = dlt > 0 && old == 0;
-                leave = dlt < 0 && old == 1;
-                outS = BAND && enter && !((swd >> (my_e & 63)) & 1ull);
+            // (my_e is a valid node on every lane: the read needs no guard, the store goes to the
+            // sink off the neighbour lanes)
+            const int old = fcnt[my_e];
+            FC_ST(is_nbr, fcnt[my_e], old + dlt);
+            const bool enter = is_nbr & (dlt > 0) & (old == 0);
+            const bool leave = is_nbr & (dlt < 0) & (old == 1);
+            bool outS = false;
+            if constexpr (BAND) {
+                const uint64_t swd = sb[my_e >> 6];
+                outS = enter && !((swd >> (my_e & 63)) & 1ull);
             }
             if (lane == 0) {
                 a[vf] = (int8_t)(1 - Af);
@@ -862,7 +868,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             uint32_t eqm = 0;
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) eqm |= (uint32_t)(cell[i] == vf) << i;
-            const bool stale = has && (v == vf || eqm != 0u);
+            const bool stale = has & ((v == vf) | (eqm != 0u));
             const uint64_t aff = __ballot(stale && lane > f && lane < end);
             if (aff) FC_PROF(13, 1);
             uint64_t ent = __ballot(enter);
@@ -904,11 +910,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             nb += dnb;
             --rem;
             last_flip = vf;
-            if (lane == f) {
-                st |= ST_VS | ST_AC;
-                cut_after = cut;
-                nb_after = nb;
-            }
+            const bool me_f = lane == f;
+            st |= me_f ? (ST_VS | ST_AC) : 0u;
+            cut_after = me_f ? cut : cut_after;
+            nb_after = me_f ? nb : nb_after;
             compiler_fence();
             FC_STAMP(t_ap1);
             FC_PROF(10, t_ap1 - t_ap0);
@@ -927,12 +932,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             }
             if (aff && pos < end) reeval(pos, vf, eqm);
         }
-        if (st & LF_WROTE) {  // clear this lane's marks for the next batch
-            smark[v] = 0xff;
-#pragma unroll
-            for (int i = 0; i < RMAX; ++i) FC_ST(((nbr >> i) & 1u), nmark[cell[i]], 0xff);
-        }
-        compiler_fence();
+        compiler_fence();  // (the marks: cleared by each segment pass)
         steps = steps0 + (rem0 - rem);
         FC_STAMP(t_d);
         FC_PROF(3, t_d - t_c);
@@ -966,13 +966,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             }
             my_wait = geom_from(u53(g.x0, g.x1), p.log1mp[nb_after]);
         }
-        if (is_acc) {
-            acc_cut += (int64_t)cut_after * run_len;
-            acc_cut2 += (int64_t)cut_after * cut_after * run_len;
-            acc_nb += (int64_t)nb_after * run_len;
-            acc_nb2 += (int64_t)nb_after * nb_after * run_len;
-            if (!defer) acc_wait += my_wait * run_len;
-        }
+        // (run_len is 0 off the accepting lanes: no guard, no exec-mask branch)
+        acc_cut += (int64_t)cut_after * run_len;
+        acc_cut2 += (int64_t)cut_after * cut_after * run_len;
+        acc_nb += (int64_t)nb_after * run_len;
+        acc_nb2 += (int64_t)nb_after * nb_after * run_len;
+        if (!defer) acc_wait += my_wait * run_len;
         if (lane == 0 && r0) {
             acc_cut += (int64_t)cut0 * r0;
             acc_cut2 += (int64_t)cut0 * cut0 * r0;

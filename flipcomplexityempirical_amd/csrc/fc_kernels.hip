@@ -269,10 +269,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                     const int nfs = (int)(pkb[v] >> 5);
                     hit = ok && ((int)(mw >> 32) < nfs || nfs == 7);
                 } else {
-                    hit = ok && (int)(mw >> 32) < (int)fcnt[v];
+                    hit = ok & ((int)(mw >> 32) < (int)fcnt[v]);  // (v < n: no guard, no branch)
                 }
             } else {
-                hit = ok && fcnt[v] != 0;
+                hit = ok & (fcnt[v] != 0);
             }
             const uint64_t hm = __ballot(hit);
             const int pos = nh + __popcll(hm & bits_below(lane));

@@ -34,6 +34,20 @@ FC_RING_HD bool one_run(uint32_t nbrA, uint32_t brk, uint32_t full) {
     return (nbrA & between) == 0u || (B & inner) == 0u;
 }
 
+// The same verdict without the early return, for the k = 2 kernel, where the early return put
+// every slot's verdict behind exec-mask branches (the k > 2 kernel keeps one_run: there this form
+// costs SGPR and VGPR spills).  With B or nbrA zero the scans see the guard bits
+// and the masks are meaningless, but the trivial case decides those inputs.
+FC_RING_HD bool one_run_flat(uint32_t nbrA, uint32_t brk, uint32_t full) {
+    const uint32_t B = brk & full;
+    const bool trivial = ((nbrA & (nbrA - 1u)) == 0u) | (B == 0u);
+    const int bmin = __builtin_ctz(B | 0x80000000u), bmax = 31 - __builtin_clz(B | 1u);
+    const int nf = __builtin_ctz(nbrA | 0x80000000u), nl = 31 - __builtin_clz(nbrA | 1u);
+    const uint32_t between = ((2u << bmax) - 1u) & ~((2u << bmin) - 1u);
+    const uint32_t inner = ((1u << nl) - 1u) & ~((1u << nf) - 1u);
+    return trivial | ((nbrA & between) == 0u) | ((B & inner) == 0u);
+}
+
 // District-graph contiguity rule (k > 2; every node exact, so each ring lists every cell that
 // shares a face with its node and the outer face is one wedge of the outer nodes' rings).
 //

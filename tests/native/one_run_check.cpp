@@ -1,4 +1,5 @@
-// Host check of the planar run rule's loop-free ring test (csrc/fc_ring.h) against its
+// Host check of the planar run rule's loop-free ring test (csrc/fc_ring.h: one_run and its
+// branch-free form one_run_flat) against its
 // statement: count the cyclic intervals between consecutive old-district neighbours that hold
 // a break; one run <=> at most one.  Exhaustive for rings of 1..10 cells, random beyond (the
 // kernels use rings of at most 16).  Prints "checked N bad B"; exit status 1 on any mismatch.
@@ -28,7 +29,8 @@ int main() {
     auto check = [&](int L, uint32_t M, uint32_t B) {
         const uint32_t full = (1u << L) - 1u;
         ++n;
-        if (fc::one_run(M, B, full) != one_run_intervals(M, B & full, full)) {
+        const bool want = one_run_intervals(M, B & full, full);
+        if (fc::one_run(M, B, full) != want || fc::one_run_flat(M, B, full) != want) {
             if (bad < 8) printf("mismatch L=%d nbrA=%x brk=%x\n", L, M, B);
             ++bad;
         }
