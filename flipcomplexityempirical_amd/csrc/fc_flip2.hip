@@ -646,39 +646,42 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     // slots), beta (later candidates), entering non-hits.  Every lane reads (cells
                     // are valid nodes on idle lanes too), so the reads issue back to back.
                     bool need = inK;
-                    int ms = 0xff, mn[RMAX], smk[RMAX], mk[NSUB];
-#pragma unroll
-                    for (int i = 0; i < RMAX; ++i) mn[i] = 0xff;
+                    // the neighbour marks only as two ring masks: cells whose mark is above / below
+                    // this lane (8 values live across the rounds made the compiler read them one
+                    // LDS round trip at a time)
+                    int ms = 0xff, mk[NSUB];
+                    uint32_t gtm = 0xffffu, ltm = 0u;
                     for (;;) {
                         FC_PROF(21, 1);
                         FC_ST(need && ms > lane, smark[v], lane);
+                        const uint32_t wm = need ? (nbr & gtm) : 0u;
 #pragma unroll
-                        for (int i = 0; i < RMAX; ++i)
-                            FC_ST(need && ((nbr >> i) & 1u) && mn[i] > lane, nmark[cell[i]], lane);
+                        for (int i = 0; i < RMAX; ++i) FC_ST((wm >> i) & 1u, nmark[cell[i]], lane);
                         compiler_fence();
                         ms = smark[v];
+                        int mn[RMAX];
 #pragma unroll
-                        for (int i = 0; i < RMAX; ++i) {
-                            mn[i] = nmark[cell[i]];
-                            smk[i] = smark[cell[i]];
-                        }
+                        for (int i = 0; i < RMAX; ++i) mn[i] = nmark[cell[i]];
 #pragma unroll
                         for (int r = 0; r < NSUB; ++r) mk[r] = nmark[rv[r] < 0 ? 0 : (rv[r] & 0xffff)];
-                        bool again = ms > lane;
+                        gtm = 0u;
+                        ltm = 0u;
 #pragma unroll
-                        for (int i = 0; i < RMAX; ++i) again |= ((nbr >> i) & 1u) && mn[i] > lane;
-                        need = need && again;
+                        for (int i = 0; i < RMAX; ++i) {
+                            gtm |= (uint32_t)(mn[i] > lane) << i;
+                            ltm |= (uint32_t)(mn[i] < lane) << i;
+                        }
+                        const bool again = (ms > lane) | ((nbr & gtm) != 0u);
+                        need = need & again;
                         if (!__any(need)) break;
                     }
                     FC_STAMP(t_mk);
                     FC_PROF(18, t_mk - t_it1);
-                    bool conf = ms < lane;
+                    // alpha: this slot's node or a ring cell is an earlier candidate's node; beta: a
+                    // neighbour shared with an earlier candidate
+                    bool conf = (ms < lane) | (inK & ((nbr & ltm) != 0u));
 #pragma unroll
-                    for (int i = 0; i < RMAX; ++i) {
-                        const bool nb_i = (nbr >> i) & 1u;
-                        conf |= smk[i] < lane;
-                        conf |= inK & nb_i & (mn[i] < lane);
-                    }
+                    for (int i = 0; i < RMAX; ++i) conf |= (int)smark[cell[i]] < lane;
                     conf &= has;
                     const uint64_t XX = __ballot(conf && lane > pos && lane < end);
                     if (XX) {
