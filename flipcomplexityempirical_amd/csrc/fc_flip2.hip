@@ -48,6 +48,8 @@ using namespace dev;
 template <int RMAX, int NSUB, bool FULL, bool SEARCH, bool XTRA, bool BAND>
 __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams p) {
     static_assert(FULL || !XTRA, "XTRA is a FULL instance");
+    // non-hit draws held per lane: the node stream's four words per Philox call, BAND's rounds
+    constexpr int kRV = BAND ? NSUB : 4;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)(threadIdx.x & 63u);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -314,38 +316,99 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // ---- 1. draws -> nodes; boundary hits packed, in draw order, into <= 64 slots ----
         int nh = 0;   // boundary hits seen
         int gen = 0;  // draws generated (offsets 0..gen-1 of this batch)
-        // this lane's non-hit draw in round r (offset 64 r + lane): node | (slots drawn before it
-        // << 16), -1: none.  "slot s precedes the draw" is then s < rv >> 16.
-        int rv[NSUB];
-        // BAND: lane l < words holds the members of S in the words below l (the rank search's keys)
-        int bpre = 0x7fffffff;
-        if constexpr (BAND) {
-            const int cw = lane < p.words ? (int)__popcll(sb[lane]) : 0;
-            const int inc = wave_scan_incl(cw);
-            if (lane < p.words) bpre = inc - cw;
-        }
-#pragma unroll
-        for (int r = 0; r < NSUB; ++r) {
-            rv[r] = -1;
-            if ((r > 0 && nh >= p.hit_stop) || nh >= 64 || (uint64_t)gen >= room) continue;
-            const int off = gen + lane;
-            const bool inrange = (uint64_t)off < room;
-            const uint64_t dr = draw + (uint64_t)off;
-            Words4 w;
+        // the nodes of this lane's non-hit draws: node | (slots drawn before it << 16), -1: none.
+        // "slot s precedes the draw" is then s < rv >> 16.  Node stream: word j of this lane's
+        // Philox call (draw offset 4 lane + j - (draw mod 4)); BAND: round j (offset 64 j + lane).
+        int rv[kRV];
+        // draw offset of entry j of lane l
+        auto rv_off = [&](int j, int l) { return BAND ? 64 * j + l : 4 * l + j - (int)(draw & 3u); };
+        if constexpr (!BAND) {
+            // node stream: the node words of draws 4q .. 4q+3 are the four words of
+            // one Philox call (ctr = q, chain, purpose 3): lane l holds q = draw / 4 + l, so one
+            // call per lane covers the batch's window of up to 64 NSUB draws, in draw order
+            // lane-major.  The acceptance words of the hits come from their own call (phase 2).
+            const int s0 = (int)(draw & 3u);
+            // (the window never passes the last lane's words: 4 * 64 - s0 draws at most)
+            const int wcap = 64 * NSUB < 4 * kWave - s0 ? 64 * NSUB : 4 * kWave - s0;
+            const int win = (uint64_t)wcap < room ? wcap : (int)room;
+            const uint64_t q = (draw >> 2) + (uint64_t)lane;
+            uint32_t nw[4];
             if (XTRA && p.tape) {
-                const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + (inrange ? dr : draw)) * 6;
-                w = Words4{t[0], t[1], t[2], t[3]};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int off = 4 * lane + j - s0;
+                    const bool inr = off >= 0 && off < win;
+                    nw[j] = p.tape[((size_t)c * (size_t)p.tape_draws + (inr ? draw + (uint64_t)off : draw)) * 6];
+                }
             } else {
-                w = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
+                const Words4 w = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), chain_gid, 3u, p.seed_lo, p.seed_hi);
+                nw[0] = w.x0;
+                nw[1] = w.x1;
+                nw[2] = w.x2;
+                nw[3] = w.x3;
             }
-            int vd;
-            bool okd;
-            if constexpr (BAND) {
+            int vdj[4];
+            uint32_t okm = 0u, hb = 0u;  // this lane's draws: Lemire-accepted, boundary hits
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int off = 4 * lane + j - s0;
+                const uint64_t m = (uint64_t)nw[j] * (uint64_t)(uint32_t)n;
+                vdj[j] = (int)(m >> 32);
+                const bool ok = (off >= 0) & (off < win) & ((uint32_t)m >= p.lemire_thresh);
+                // (vdj < n on every lane: the read needs no guard)
+                okm |= (uint32_t)ok << j;
+                hb |= (uint32_t)(ok & (fcnt[vdj[j]] != 0)) << j;
+            }
+            const int hc = __popc(hb);
+            const int incl = wave_scan_incl(hc);
+            const int excl = incl - hc;
+            const int tot = rl32(incl, kWave - 1);
+            gen = win;
+            int lim = 4 * kWave;  // draws of the window consumed, as an offset bound
+            if (tot > 64) {  // the 64th hit closes the batch
+                const int L = __builtin_ctzll(__ballot(incl >= 64));
+                const uint32_t hbL = rlu(hb, L);
+                const int k = 64 - rl32(excl, L);  // its rank among lane L's hits (1-based)
+                uint32_t mk = hbL;  // its word: the k-th set bit of lane L's hits (wave-uniform)
+                for (int i = 1; i < k; ++i) mk &= mk - 1u;
+                const int jj = __builtin_ctz(mk);
+                lim = 4 * L + jj - s0 + 1;
+                gen = lim;
+            }
+            // the slot lanes' sink for masked-off stores: row 4 of the slots (phase 2 writes it)
+            uint32_t *const ssink = slot + 256 + lane;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int off = 4 * lane + j - s0;
+                const int sp = excl + __popc(hb & ((1u << j) - 1u));
+                const bool hit = (hb >> j) & 1u;
+                const bool put = hit & (sp < 64);
+                *(put ? slot + sp : ssink) = (uint32_t)vdj[j];
+                *(put ? slot + 192 + sp : ssink) = (uint32_t)off;
+                rv[j] = (((okm >> j) & 1u) & !hit & (off < lim)) ? (vdj[j] | (sp << 16)) : -1;
+            }
+            nh = tot;
+        } else {
+            // BAND: lane l < words holds the members of S in the words below l (the rank search's keys)
+            int bpre = 0x7fffffff;
+            {
+                const int cw = lane < p.words ? (int)__popcll(sb[lane]) : 0;
+                const int inc = wave_scan_incl(cw);
+                if (lane < p.words) bpre = inc - cw;
+            }
+#pragma unroll
+            for (int r = 0; r < NSUB; ++r) {
+                rv[r] = -1;
+                if ((r > 0 && nh >= p.hit_stop) || nh >= 64 || (uint64_t)gen >= room) continue;
+                const int off = gen + lane;
+                const bool inrange = (uint64_t)off < room;
+                const uint64_t dr = draw + (uint64_t)off;
+                const Words4 w = philox4x32_10((uint32_t)dr, (uint32_t)(dr >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
                 // exact Lemire over |S|, then the idx-th member of S: the word by a binary search
                 // over the lanes' prefix counts, the bit by popcount halvings
                 const uint64_t m = (uint64_t)w.x0 * (uint64_t)nS;
                 const int idx = (int)(m >> 32);
-                okd = inrange && (uint32_t)m >= thrS;
+                const bool okd = inrange && (uint32_t)m >= thrS;
                 int bw = 0, bb = 0;
                 for (int st2 = p.band_step0; st2 >= 1; st2 >>= 1) {
                     const int cand = bw + st2;
@@ -355,33 +418,27 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         bb = pc;
                     }
                 }
-                vd = 64 * bw + select_bit64(sb[bw], idx - bb);
-            } else {
-                const uint64_t m = (uint64_t)w.x0 * (uint64_t)(uint32_t)n;
-                vd = (int)(m >> 32);
-                okd = inrange && (uint32_t)m >= p.lemire_thresh;
+                const int vd = 64 * bw + select_bit64(sb[bw], idx - bb);
+                const bool hitd = okd & (fcnt[vd] != 0);
+                const uint64_t hm = __ballot(hitd);
+                const int sp = nh + count_below(hm);
+                if (hitd && sp < 64) {
+                    slot[sp] = (uint32_t)vd;
+                    slot[64 + sp] = w.x1;
+                    slot[128 + sp] = w.x2;
+                    slot[192 + sp] = (uint32_t)off;
+                }
+                const int cnt = __popcll(hm);
+                int used = kWave;  // lanes of this round consumed by the batch
+                if (nh + cnt > 64) {  // the 64th hit closes the batch inside this round
+                    used = kth_set_bit(hm, 64 - nh) + 1;
+                    gen += used;
+                } else {
+                    gen = (uint64_t)(gen + 64) < room ? gen + 64 : (int)room;
+                }
+                rv[r] = (okd & !hitd & (lane < used)) ? (vd | (sp << 16)) : rv[r];
+                nh += cnt;
             }
-            // (vd < n for every lane: the read needs no guard, and a short-circuit && would put it
-            // behind an exec-mask branch)
-            const bool hitd = okd & (fcnt[vd] != 0);
-            const uint64_t hm = __ballot(hitd);
-            const int sp = nh + count_below(hm);
-            if (hitd && sp < 64) {
-                slot[sp] = (uint32_t)vd;
-                slot[64 + sp] = w.x1;
-                slot[128 + sp] = w.x2;
-                slot[192 + sp] = (uint32_t)off;
-            }
-            const int cnt = __popcll(hm);
-            int used = kWave;  // lanes of this round consumed by the batch
-            if (nh + cnt > 64) {  // the 64th hit closes the batch inside this round
-                used = kth_set_bit(hm, 64 - nh) + 1;
-                gen += used;
-            } else {
-                gen = (uint64_t)(gen + 64) < room ? gen + 64 : (int)room;
-            }
-            rv[r] = (okd & !hitd & (lane < used)) ? (vd | (sp << 16)) : rv[r];
-            nh += cnt;
         }
         const int ns = nh < 64 ? nh : 64;
         compiler_fence();
@@ -395,7 +452,25 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         int off_l = has ? off_r : gen;
         const uint64_t d = draw + (uint64_t)off_l;
         int v = has ? v_r : 0;
-        const uint32_t w1 = slot[64 + lane], w2 = slot[128 + lane];
+        uint32_t w1, w2;  // the draw's acceptance words (random(), grid_chain_sec11.py:179)
+        if constexpr (BAND) {
+            w1 = slot[64 + lane];
+            w2 = slot[128 + lane];
+        } else {
+            // node stream: words 1-2 of the draw's own Philox call (ctr = draw, chain, purpose 0),
+            // made for the hits only; kept in the slots for the re-evaluations
+            if (XTRA && p.tape) {
+                const uint32_t *t = p.tape + ((size_t)c * (size_t)p.tape_draws + (has ? d : draw)) * 6;
+                w1 = t[1];
+                w2 = t[2];
+            } else {
+                const Words4 g = philox4x32_10((uint32_t)d, (uint32_t)(d >> 32), chain_gid, 0u, p.seed_lo, p.seed_hi);
+                w1 = g.x1;
+                w2 = g.x2;
+            }
+            slot[64 + lane] = w1;
+            slot[128 + lane] = w2;
+        }
         const NodeRec<RMAX> rec = G[v];
         int av = a[v];
         int pv = rec.pop;
@@ -649,7 +724,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     // the neighbour marks only as two ring masks: cells whose mark is above / below
                     // this lane (8 values live across the rounds made the compiler read them one
                     // LDS round trip at a time)
-                    int ms = 0xff, mk[NSUB];
+                    int ms = 0xff, mk[kRV];
                     uint32_t gtm = 0xffffu, ltm = 0u;
                     for (;;) {
                         FC_PROF(21, 1);
@@ -663,7 +738,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
 #pragma unroll
                         for (int i = 0; i < RMAX; ++i) mn[i] = nmark[cell[i]];
 #pragma unroll
-                        for (int r = 0; r < NSUB; ++r) mk[r] = nmark[rv[r] < 0 ? 0 : (rv[r] & 0xffff)];
+                        for (int r = 0; r < kRV; ++r) mk[r] = nmark[rv[r] < 0 ? 0 : (rv[r] & 0xffff)];
                         gtm = 0u;
                         ltm = 0u;
 #pragma unroll
@@ -694,10 +769,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     // first of them
                     int t = trunc_off;
 #pragma unroll
-                    for (int r = 0; r < NSUB; ++r) {
+                    for (int r = 0; r < kRV; ++r) {
                         const bool tr = (rv[r] >= 0) & (mk[r] < x) & (mk[r] < (rv[r] >> 16));
                         const uint64_t TR = __ballot(tr);
-                        if (TR) t = min(t, 64 * r + __builtin_ctzll(TR));
+                        if (TR) t = min(t, rv_off(r, __builtin_ctzll(TR)));
                     }
                     if (t < trunc_off) {
                         trunc_off = t;
@@ -881,14 +956,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             // when it was drawn, and a flip before f that gave it one has cut the batch already)
             if (ent) {
                 int t_na = trunc_off;
-                int fr[NSUB];
+                int fr[kRV];
 #pragma unroll
-                for (int r = 0; r < NSUB; ++r) fr[r] = fcnt[rv[r] < 0 ? 0 : (rv[r] & 0xffff)];
+                for (int r = 0; r < kRV; ++r) fr[r] = fcnt[rv[r] < 0 ? 0 : (rv[r] & 0xffff)];
 #pragma unroll
-                for (int r = 0; r < NSUB; ++r) {
+                for (int r = 0; r < kRV; ++r) {
                     const bool tr = (rv[r] >= 0) & ((rv[r] >> 16) > f) & (fr[r] != 0);
                     const uint64_t m2 = __ballot(tr);
-                    if (m2) t_na = min(t_na, 64 * r + __builtin_ctzll(m2));
+                    if (m2) t_na = min(t_na, rv_off(r, __builtin_ctzll(m2)));
                 }
                 if (t_na < trunc_off) {
                     trunc_off = t_na;

@@ -163,6 +163,15 @@ static void draw_words(const fr_params *p, int64_t d, uint32_t purpose, uint32_t
     uint32_t ctr[4] = {(uint32_t)(uint64_t)d, (uint32_t)((uint64_t)d >> 32), p->chain_id, purpose};
     uint32_t key[2] = {(uint32_t)p->seed, (uint32_t)(p->seed >> 32)};
     fr_philox4x32_10(ctr, key, w);
+    if (purpose == 0 && p->k == 2 && p->stream == FR_STREAM_NODE) {
+        /* k = 2 node stream: the node word of draw d is word d mod 4 of the
+         * purpose-3 call at counter d / 4 (four draws' node words per call); words 1-3 stay the
+         * draw's own (the device makes that call for the boundary hits only). */
+        const uint64_t q = (uint64_t)d >> 2;
+        uint32_t cq[4] = {(uint32_t)q, (uint32_t)(q >> 32), p->chain_id, 3u}, wq[4];
+        fr_philox4x32_10(cq, key, wq);
+        w[0] = wq[d & 3];
+    }
 }
 
 /* geom_wait (grid_chain_sec11.py:147-148): int(np.random.geometric(p, 1)) - 1 with the

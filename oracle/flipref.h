@@ -15,7 +15,9 @@
  * Random stream (the shared canonical spec, see DESIGN.md "Random stream"): draw d of
  * chain c uses Philox4x32-10(ctr = (lo32 d, hi32 d, c, 0), key = (lo32 seed, hi32 seed)).
  * Node = Lemire multiply-shift of word 0 over N (exact: reject low < 2^32 mod N); a draw
- * whose node is not a boundary node is not a proposal.  Band stream (FR_STREAM_BAND): the
+ * whose node is not a boundary node is not a proposal.  k = 2 node stream: word 0 of draw d is
+ * instead word d mod 4 of Philox(ctr = (lo32 q, hi32 q, c, 3)), q = d / 4 (four draws' node
+ * words per call; words 1-3 stay the draw's own).  Band stream (FR_STREAM_BAND): the
  * same map over |S| picks the i-th node of the band S in ascending order instead.  Acceptance U53 = CPython random()
  * from words (1, 2).  The geometric wait of the state created by draw d uses purpose 1,
  * the initial state's purpose 2 at d = 0; U53 from words (0, 1).

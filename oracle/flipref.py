@@ -57,15 +57,25 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
     return tuple(np.asarray(x, dtype=np.uint32) for x in (c0, c1, c2, c3))
 
 
-def draw_tape(seed: int, chain_id: int, n_draws: int, start: int = 0) -> np.ndarray:
+def node_words_k2(seed: int, chain_id: int, d) -> np.ndarray:
+    """k = 2 node stream (flipref.c draw_words): the node word of draw d is word d mod 4 of the
+    purpose-3 Philox call at counter d // 4."""
+    d = np.asarray(d, dtype=np.uint64)
+    q = d >> np.uint64(2)
+    w = philox4x32_10(q & MASK32, q >> np.uint64(32), chain_id, 3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    return np.choose((d & np.uint64(3)).astype(np.int64), w).astype(np.uint32)
+
+
+def draw_tape(seed: int, chain_id: int, n_draws: int, start: int = 0, k: int = 2) -> np.ndarray:
     """The canonical stream as an explicit tape: 6 u32 per draw (4 proposal words, then the
-    2 geometric-wait words of purpose 1)."""
+    2 geometric-wait words of purpose 1); k = 2 takes word 0 from the four-per-call node stream."""
     d = np.arange(start, start + n_draws, dtype=np.uint64)
     lo, hi = d & MASK32, d >> np.uint64(32)
     k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
     a = philox4x32_10(lo, hi, chain_id, 0, k0, k1)
     g = philox4x32_10(lo, hi, chain_id, 1, k0, k1)
-    tape = np.stack([a[0], a[1], a[2], a[3], g[0], g[1]], axis=1)
+    w0 = node_words_k2(seed, chain_id, d) if k == 2 else a[0]
+    tape = np.stack([w0, a[1], a[2], a[3], g[0], g[1]], axis=1)
     return np.ascontiguousarray(tape.reshape(-1), dtype=np.uint32)
 
 
@@ -428,9 +438,11 @@ class GcFaithfulChain:
         if self.tape is not None and purpose != 2:
             t = self.tape[6 * d: 6 * d + 6]
             return [int(x) for x in (t[:4] if purpose == 0 else t[4:6])]
-        w = philox4x32_10(d & 0xFFFFFFFF, d >> 32, self.chain_id, purpose,
-                          self.seed & 0xFFFFFFFF, self.seed >> 32)
-        return [int(x) for x in w]
+        w = [int(x) for x in philox4x32_10(d & 0xFFFFFFFF, d >> 32, self.chain_id, purpose,
+                                            self.seed & 0xFFFFFFFF, self.seed >> 32)]
+        if purpose == 0 and len(self.labels) == 2 and not self.band:  # k = 2 node stream
+            w[0] = int(node_words_k2(self.seed, self.chain_id, d))
+        return w
 
     def _geom(self, d, purpose):
         if self.log1mp is None:
