@@ -1045,10 +1045,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             my_wait = geom_from(u53(g.x0, g.x1), p.log1mp[nb_after]);
         }
         // (run_len is 0 off the accepting lanes: no guard, no exec-mask branch)
-        acc_cut += (int64_t)cut_after * run_len;
-        acc_cut2 += (int64_t)cut_after * cut_after * run_len;
-        acc_nb += (int64_t)nb_after * run_len;
-        acc_nb2 += (int64_t)nb_after * nb_after * run_len;
+        {
+            const int cr = cut_after * run_len, br = nb_after * run_len;  // < 2^31: |cut| < 2^24, runs <= 64
+            acc_cut += cr;
+            acc_cut2 += (int64_t)cr * cut_after;
+            acc_nb += br;
+            acc_nb2 += (int64_t)br * nb_after;
+        }
         if (!defer) acc_wait += my_wait * run_len;
         if (lane == 0 && r0) {
             acc_cut += (int64_t)cut0 * r0;
