@@ -124,6 +124,32 @@ def test_tape_replay_matches_philox(gpu, cref, sec11):
         _check_chain(cref, sec11, run_w, c, inits[c], bases[c], steps=800, tape=wild[c])
 
 
+@pytest.mark.parametrize("cap", [1, 255, 1001, 4099])
+def test_k2_node_stream_draw_cap(gpu, cref, sec11, cap):
+    """The four-per-call node stream when the launch's draw cap falls inside a
+    batch window (and at 1 draw): the device stops at the cap exactly where the oracle does --
+    every proposal, every counter (draws included), the final state and the stuck flag."""
+    inits, bases = _configs(sec11, G.sec11_plan, [0.5, 10.0], 6)
+    (_, _), (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 2, 0.1)
+    fg = FlipGraph(sec11)
+    cfg = RunConfig(seed=11, pop_lo=lo, pop_hi=hi, diag_mask=ALL_DIAG, trace_chains=6, trace_cap=200000)
+    run = FlipRun(fg, inits, cfg, bases=bases)
+    run.steps(10 ** 6, max_draws=cap)
+    st = run.stats()
+    for c in range(6):
+        ref = cref.run(sec11, inits[c], base=bases[c], pop_lo=lo, pop_hi=hi, seed=11, chain_id=c, n_steps=10 ** 6,
+                       log1mp=G.log1mp_table(sec11.n, 2), trace_cap=200000, max_draws=cap)
+        tr, rt = run.trace(c), ref["trace"]
+        assert len(tr) == len(rt), (c, len(tr), len(rt))
+        for f in ("draw", "v", "flags", "cut", "nb", "wait"):
+            assert np.array_equal(tr[f], rt[f]), (c, f)
+        for k in STAT_KEYS:
+            assert int(st[k][c]) == int(ref["stats"][k]), (c, k)
+        assert int(st["stuck"][c]) == 1 and int(ref["stats"]["stuck"]) == 1, c
+        assert np.array_equal(run.state()[c], ref["final"]), c
+    run.close()
+
+
 def test_c1_grid10(gpu, cref):
     """BASELINE config C1 at its configured length: 10x10 grid, plan x[0] >= 5, base 1
     (lambda = 1), pop tolerance 0.1, one chain of 1e5 yields (99,999 steps after S0), plus the
