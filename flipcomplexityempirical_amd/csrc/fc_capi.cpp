@@ -478,7 +478,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         if (t.deal != 1 && t.deal != -1) return fail(FC_ERR_ARG, "fc_run_create: tune_deal must be 1 or -1");
         t.deal = t.deal > 0 && k == 2 && !recom;
         const bool th_default = p->tune_prio_th[0] == 0.0f && p->tune_prio_th[1] == 0.0f && p->tune_prio_th[2] == 0.0f;
-        const float th0[3] = {0.9f, 1.0f, 1.1f};
+        const float th0[3] = {0.95f, 1.0f, 1.05f};  // tools/gpu_knobs_r04.sh: 55.3 against 55.8 ms at {0.9, 1.0, 1.1}
         for (int i = 0; i < 3; ++i) t.prio_th[i] = th_default ? th0[i] : p->tune_prio_th[i];
     }
 

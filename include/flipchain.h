@@ -153,7 +153,7 @@ typedef struct fc_params {
                                    n / div (default {2, 5, 10}); tune_prio_div[0] < 0: off      */
     float tune_prio_th[3];      /* ... and, once a chain has taken 1/16 of the launch's steps,
                                    for projected finish / previous launch's slowest above these
-                                   (default {0.9, 1.0, 1.1}); tune_prio_th[0] < 0: |B| rule only */
+                                   (default {0.95, 1.0, 1.05}); tune_prio_th[0] < 0: |B| rule only */
     int32_t tune_search_waves;  /* k > 2, chains of more than 16 KB LDS whose contiguity needs the
                                    device search (no district-graph rule): 4 = one chain per
                                    256-thread workgroup, searches by the whole workgroup;
