@@ -45,6 +45,10 @@ using namespace dev;
 // neighbours, an LDS bitmap) instead of one of all n nodes.  S only changes when an accepted flip
 // puts a node outside S into b_nodes; the batch then ends after that flip and S is rebuilt, so
 // within a batch the draw -> node map is fixed, as the speculative evaluation needs.
+// the issue priority is re-chosen every 2^FC_PRIO_EVERY_LOG2 batches (scheduling only)
+#ifndef FC_PRIO_EVERY_LOG2
+#define FC_PRIO_EVERY_LOG2 4  // profiles/r04p_prio_period_ab.txt: 55.0 ms against 55.4 every 4 batches, 56.3 every batch
+#endif
 template <int RMAX, int NSUB, bool FULL, bool SEARCH, bool XTRA, bool BAND>
 __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams p) {
     static_assert(FULL || !XTRA, "XTRA is a FULL instance");
@@ -276,7 +280,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         qn = 0;
         compiler_fence();
     };
-    int prio = 0;  // bits 0-1: the issue priority set; bits 2-3: batches since it was last chosen
+    int prio = 0;  // bits 0-1: the issue priority set; bits 2 and up: batches since it was last chosen
     if (lane == 0) {
         misc[0] = __builtin_amdgcn_s_memrealtime();
         // the previous launch's slowest-chain pace, scaled to this launch (0: none yet)
@@ -285,8 +289,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     }
     compiler_fence();
     while (rem > 0) {
-        // re-chosen every fourth batch (it moves slowly; scheduling only)
-        if (p.prio_nb[0] > 0 && ((prio += 4) & 12) == 0) {
+        // re-chosen every 2^FC_PRIO_EVERY_LOG2 batches (it moves slowly; scheduling only)
+        if (p.prio_nb[0] > 0 && ((prio += 4) & (((1 << FC_PRIO_EVERY_LOG2) - 1) << 2)) == 0) {
             const int done = (int)p.n_steps - rem;
             const float eta = __uint_as_float((uint32_t)misc[1]);
             int lv;
