@@ -8,10 +8,11 @@
 //
 // One chain per wavefront, state in LDS (int8 district, uint8 foreign-neighbour count per
 // node; |B| and boundary membership are O(1)).  A wave advances its chain in batches:
-//   1. up to NSUB rounds of 64 Philox draws map to nodes (exact Lemire); draws on boundary
-//      nodes are proposals (rejection sampling of random.choice over b_nodes,
-//      grid_chain_sec11.py:143) and are packed, in draw order, into up to 64 slots; the
-//      nodes of the other ("non-hit") draws stay in registers;
+//   1. a window of up to 64 NSUB draws maps to nodes (exact Lemire; the node words of four
+//      draws come from one Philox call per lane); draws on boundary nodes are
+//      proposals (rejection sampling of random.choice over b_nodes, grid_chain_sec11.py:143)
+//      and are packed, in draw order, into up to 64 slots; the nodes of the other ("non-hit")
+//      draws stay in registers;
 //   2. every slot is evaluated against the current state: ring districts, contiguity by the
 //      planar run rule, population bound, delta-cut, Metropolis threshold;
 //   3. commit in draw order.  One event at a time when few slots of the batch accept: the

@@ -138,11 +138,12 @@ typedef struct fc_params {
     /* Launch tuning.  Scheduling only: no trajectory, statistic or trace depends on these
      * (tests/test_parity_gpu.py::test_sec11_batch_shapes, test_pair_gpu.py::test_k4_wait_queue_lengths). 0 = the default;
      * the library reads no environment variables.                                          */
-    int32_t tune_nsub;          /* draw rounds of 64 per batch, in {1, 2, 4}: k = 2 default 4;
-                                   k > 2 default 2 (4 when the slot bound wmax exceeds 8);
-                                   anything else FC_ERR_ARG                                    */
-    int32_t tune_hit_stop;      /* no further draw round once a batch holds this many boundary
-                                   hits (default 32)                                           */
+    int32_t tune_nsub;          /* draws per batch in units of 64, in {1, 2, 4}: k = 2 default 4
+                                   (a window of 64 nsub draws, four node words per Philox call;
+                                   band stream: rounds of 64); k > 2 default 2 (4 when the slot
+                                   bound wmax exceeds 8); anything else FC_ERR_ARG              */
+    int32_t tune_hit_stop;      /* rounds of 64 (k > 2, k = 2 band stream): no further round
+                                   once a batch holds this many boundary hits (default 32)     */
     int32_t tune_par_min;       /* k = 2: segment-parallel commit from this many acceptances on
                                    (default 3; > 64 = one event at a time)                     */
     int32_t tune_wait_queue;    /* accepted states queued for their geometric wait before one
