@@ -54,10 +54,12 @@ __device__ __forceinline__ int wave_scan_incl(int x) {
     x += dpp_mov<0x112>(x);
     x += dpp_mov<0x114>(x);
     x += dpp_mov<0x118>(x);
-    const int r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31),
-              r2 = __builtin_amdgcn_readlane(x, 47);
-    const int lane = (int)__lane_id();
-    return x + (lane >= 16 ? r0 : 0) + (lane >= 32 ? r1 : 0) + (lane >= 48 ? r2 : 0);
+    // row totals by the row broadcasts: row_bcast:15 adds lane 15 to row 1 and lane 47 to row
+    // 3 (row mask 0xa), then row_bcast:31 adds lane 31 to rows 2 and 3 (row mask 0xc); two DPP
+    // adds instead of three readlanes and their selects
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+    return x;
 }
 
 // position of the r-th (0-based) set bit of x, r < popcount(x): five popcount halvings
