@@ -487,11 +487,18 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         // districts are 0 / 1: pack the ring's district-1 bits, then A's bits are those or
         // their complement (shift-ors, no compare / select per cell)
         uint32_t in1 = 0;
+        int ad[RMAX];
 #pragma unroll
         for (int i = 0; i < RMAX; ++i) {
             cell[i] = ring_entry<RMAX>(rec.ring, i);
-            in1 |= (uint32_t)a[cell[i]] << i;
+            ad[i] = a[cell[i]];
         }
+        // every read issued before the first use (the compiler otherwise waited on each read
+        // before issuing the next: eight LDS round trips in a row)
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) asm volatile("" : "+v"(ad[i]));
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) in1 |= (uint32_t)ad[i] << i;
         uint32_t inA = (av ? in1 : ~in1) & full;
         slot[256 + lane] = link | (Ln << 16);  // for re-evaluations inside the commit
         // target district: 1 - av (-1 * assignment, grid_chain_sec11.py:145)
@@ -554,8 +561,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 if (vfx < 0) {
                     av = a[v];
                     uint32_t i1 = 0;
+                    int ad[RMAX];
 #pragma unroll
-                    for (int i = 0; i < RMAX; ++i) i1 |= (uint32_t)a[cell[i]] << i;
+                    for (int i = 0; i < RMAX; ++i) ad[i] = a[cell[i]];
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i) asm volatile("" : "+v"(ad[i]));  // (reads issued together)
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i) i1 |= (uint32_t)ad[i] << i;
                     inA = av ? i1 : ~i1;
                 } else {
                     const bool self = v == vfx;  // its own node flipped: every ring relation inverts
@@ -831,12 +843,15 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     compiler_fence();
                     int dnb = 0;
                     // (bit masks, not short-circuit tests: those compiled to a branch per cell)
-                    const uint32_t nbm = me ? nbr : 0u, upm = inA & nbm, dnm = tmask & nbm;
+                    // two districts: a neighbour in A gains v as a foreign neighbour (+1), one in T
+                    // loses it (-1); |B| changes by the neighbours whose count leaves or reaches 0
+                    const uint32_t nbm = me ? nbr : 0u;
 #pragma unroll
                     for (int i = 0; i < RMAX; ++i) {
-                        const uint32_t up = (upm >> i) & 1u, dn = (dnm >> i) & 1u;  // dlt = up - dn
-                        FC_ST((nbm >> i) & 1u, fcnt[cell[i]], oldc[i] + (int)up - (int)dn);
-                        dnb += (int)(up & (uint32_t)(oldc[i] == 0)) - (int)(dn & (uint32_t)(oldc[i] == 1));
+                        const int nw = oldc[i] + 2 * (int)((inA >> i) & 1u) - 1;
+                        const uint32_t nb_i = (nbm >> i) & 1u;
+                        FC_ST(nb_i, fcnt[cell[i]], nw);
+                        dnb += (min(nw, 1) - min(oldc[i], 1)) & -(int)nb_i;
                     }
                     FC_ST(me, *(uint8_t *)&a[v], 1 - av);
                     FC_ST(me, fcnt[v], nA);
