@@ -331,11 +331,20 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
             tmask = nbr & ~inA;
         } else {
             uint32_t dall = 0;                  // districts among the neighbours
+            // the raw bytes first, every read issued before the first use (the compiler otherwise
+            // waited on each), then the districts
 #pragma unroll
             for (int i = 0; i < RMAX; ++i) {
-                adv[i] = dist(ring_entry<RMAX>(rec.ring, i));
+                const int u = ring_entry<RMAX>(rec.ring, i);
+                adv[i] = PK ? (int)pkb[u] : (int)a[u];
+            }
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) asm volatile("" : "+v"(adv[i]));
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) {
+                if constexpr (PK) adv[i] &= 31;
                 inA |= (uint32_t)(adv[i] == av) << i;
-                if ((nbr >> i) & 1u) dall |= 1u << adv[i];
+                dall |= (((nbr >> i) & 1u) << adv[i]);
             }
             const uint32_t dm = dall & ~(1u << av);  // foreign districts among the neighbours
             inA &= full;
@@ -692,14 +701,24 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                         au_m = dist(um);
                         const uint32_t nbu = (uint32_t)(ru.meta >> kMetaNbrShift) & 0xffffu;
                         uint32_t du = 0, du0 = 0;
+                        // every ring cell read (valid nodes), all issued before the first use;
+                        // the neighbour bit masks the district bit in
+                        int xr[RMAX];
 #pragma unroll
-                        for (int k = 0; k < RMAX; ++k)
-                            if ((nbu >> k) & 1u) {
-                                const int w = ring_entry<RMAX>(ru.ring, k);
-                                const int xw = w == vm ? Tm : dist(w);
-                                du |= 1u << xw;
-                                du0 |= 1u << (w == vm ? Am : xw);
-                            }
+                        for (int k = 0; k < RMAX; ++k) {
+                            const int w = ring_entry<RMAX>(ru.ring, k);
+                            xr[k] = PK ? (int)pkb[w] : (int)a[w];
+                        }
+#pragma unroll
+                        for (int k = 0; k < RMAX; ++k) asm volatile("" : "+v"(xr[k]));
+#pragma unroll
+                        for (int k = 0; k < RMAX; ++k) {
+                            const int w = ring_entry<RMAX>(ru.ring, k);
+                            const uint32_t nk = (nbu >> k) & 1u;
+                            const int xd = PK ? (xr[k] & 31) : xr[k];
+                            du |= nk << (w == vm ? Tm : xd);
+                            du0 |= nk << (w == vm ? Am : xd);
+                        }
                         nfn_m = __popc(du & ~(1u << au_m));
                         old_m = __popc(du0 & ~(1u << au_m));
                     }
@@ -933,14 +952,23 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                     const int au = dist(my_e);
                     const uint32_t nbu = (uint32_t)(ru.meta >> kMetaNbrShift) & 0xffffu;
                     uint32_t du = 0, du0 = 0;  // districts among u's neighbours after / before the flip
+                    // (every ring cell read, the reads issued together; the neighbour bit masks)
+                    int xr[RMAX];
 #pragma unroll
-                    for (int i = 0; i < RMAX; ++i)
-                        if ((nbu >> i) & 1u) {
-                            const int w = ring_entry<RMAX>(ru.ring, i);
-                            const int xw = dist(w);
-                            du |= 1u << xw;
-                            du0 |= 1u << (w == vf ? Af : xw);
-                        }
+                    for (int i = 0; i < RMAX; ++i) {
+                        const int w = ring_entry<RMAX>(ru.ring, i);
+                        xr[i] = PK ? (int)pkb[w] : (int)a[w];
+                    }
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i) asm volatile("" : "+v"(xr[i]));
+#pragma unroll
+                    for (int i = 0; i < RMAX; ++i) {
+                        const int w = ring_entry<RMAX>(ru.ring, i);
+                        const uint32_t ni = (nbu >> i) & 1u;
+                        const int xw = PK ? (xr[i] & 31) : xr[i];
+                        du |= ni << xw;
+                        du0 |= ni << (w == vf ? Af : xw);
+                    }
                     const int nfn = __popc(du & ~(1u << au));
                     // the old count: exact from the ring when packed (a stored 7 may stand for more)
                     const int old = PK ? __popc(du0 & ~(1u << au)) : (int)fcnt[my_e];
