@@ -347,8 +347,9 @@ def spawn_probe():
 
 def _cpu_worker(args):
     """One chain of the same workload on a gerrychain-faithful Python port: ``native`` is
-    the reference's own proposal mechanism (``random.choice(list(b_nodes))``, :143, with
-    CPython / numpy Mersenne Twisters), ``philox`` the canonical-stream port."""
+    the reference's own proposal mechanism (``random.choice(list(b_nodes))``, :143, or for
+    k > 2 ``random.choice`` over the (node, district) pairs, :128 / :151-153, with CPython /
+    numpy Mersenne Twisters), ``philox`` the canonical-stream port."""
     gid, seconds, wname, kind = args
     sys.path.insert(0, ROOT)
     from flipcomplexityempirical_amd import graphs as G
@@ -360,7 +361,7 @@ def _cpu_worker(args):
     (lo, hi), _ = G.population_bounds(int(spec.pop.sum()), w.k, w.pct)
     if kind == "native":
         ch = NativeRngChain(spec, plan, base=w.base_of(gid), pop_bounds=(lo, hi), seed=w.seed * 1000003 + gid,
-                            log1mp=G.log1mp_table(spec.n, w.k))
+                            log1mp=G.log1mp_table(spec.n, w.k), pair=w.k > 2)
     else:
         ch = GcFaithfulChain(spec, plan, base=w.base_of(gid), pop_bounds=(lo, hi), seed=w.seed,
                              chain_id=gid, log1mp=G.log1mp_table(spec.n, w.k), pair=w.k > 2)
@@ -420,8 +421,11 @@ def cpu_baseline(seconds: float, cores: int, wname: str = "c2", kind: str = "nat
     props = sum(r[0] for r in res)
     wall = max(r[2] for r in res)
     what = ("the reference's flip step under its own random streams (oracle/flipref.py NativeRngChain: "
-            "random.choice(list(b_nodes)) at grid_chain_sec11.py:143, random() at :179, np.random.geometric "
-            "at :148, gerrychain-0.2 Partition / cut_edges / Dijkstra contiguity)" if kind == "native" else
+            + ("random.choice(list(b_nodes)) at grid_chain_sec11.py:143" if Workload(wname).k == 2 else
+               "random.choice over the (node, district) pairs of slow_reversible_propose, grid_chain_sec11.py:128 "
+               "over :151-153")
+            + ", random() at :179, np.random.geometric at :148, gerrychain-0.2 Partition / cut_edges / Dijkstra "
+            "contiguity)" if kind == "native" else
             "gerrychain-0.2-faithful Python restatement on the canonical Philox stream "
             "(oracle/flipref.py GcFaithfulChain)")
     return {"value": props / wall, "unit": "proposals/s", "cores": cores, "kind": "port",
@@ -855,12 +859,14 @@ def main():
         out["reference_sweeps"] = sweep_leg(args.sweep_replicas, local_rank)
     if node_out is not None:
         out["node_stream"] = node_out
-    if world == 1 and not args.no_cpu_baseline:
-        # one process per CPU this job can use: every host core, unless the affinity set or a
-        # cgroup quota grants fewer (then the host's figure is stated as an extrapolation)
+    if not args.no_cpu_baseline:
+        # rank 0 only (the other ranks have left), after every collective and outside the timed
+        # region, so an N-GPU line carries its CPU baseline too: one process per CPU this job can
+        # use -- every host core, unless the affinity set or a cgroup quota grants fewer (then the
+        # host's figure is stated as an extrapolation)
         cores, share = host_cpu_share()
         try:
-            kind = "native" if W.k == 2 else "philox"
+            kind = "native"
             cb = cpu_baseline(args.cpu_seconds, cores, args.workload, kind)
             cb.update(share)
             cb["cores_note"] = ("one process per usable CPU: os.sched_getaffinity, capped by the cgroup CPU quota; "

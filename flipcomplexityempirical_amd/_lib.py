@@ -39,7 +39,7 @@ EXPORTED = [
     "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
     "fc_run_frame_series", "fc_run_frame_series_changes", "fc_host_register", "fc_host_unregister",
     "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_destroy",
-    "fc_device_count", "fc_last_error", "fc_build_flags",
+    "fc_device_count", "fc_last_error", "fc_build_flags", "fc_build_id",
 ]
 
 FC_BUILD_PHASE_PROF, FC_BUILD_PHASE_SYNC, FC_BUILD_VARIANT = 0x1, 0x2, 0x4  # include/flipchain.h
@@ -121,6 +121,11 @@ def build_flags() -> int:
     return int(load().fc_build_flags())
 
 
+def build_id() -> str:
+    """``fc_build_id()`` of the loaded library: the content hash of the sources it was built from."""
+    return load().fc_build_id().decode()
+
+
 def load(build_if_missing: bool = True, allow_variant: bool = False):
     """Load (building if needed) the native library; raises when it cannot be had.
 
@@ -197,9 +202,11 @@ def load(build_if_missing: bool = True, allow_variant: bool = False):
     L.fc_last_error.restype = ctypes.c_char_p
     L.fc_build_flags.argtypes = []
     L.fc_build_flags.restype = ctypes.c_uint32
+    L.fc_build_id.argtypes = []
+    L.fc_build_id.restype = ctypes.c_char_p
     for name in EXPORTED:
         if name not in ("fc_graph_destroy", "fc_run_destroy", "fc_last_error", "fc_run_n_chains",
-                        "fc_run_chain_lds_bytes", "fc_build_flags"):
+                        "fc_run_chain_lds_bytes", "fc_build_flags", "fc_build_id"):
             getattr(L, name).restype = ctypes.c_int
     bf = int(L.fc_build_flags())
     if bf and not _allow_variant:

@@ -5,7 +5,9 @@ repository snapshot.  ``python -m flipcomplexityempirical_amd.build`` rebuilds i
 """
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import subprocess
 import sys
 import tempfile
@@ -26,12 +28,47 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("FC_OFFLOAD_ARCH", "gfx950")
 
 
+def _flags() -> list:
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+    for tok in filter(None, VARIANT.split("_")):
+        if tok not in VARIANT_FLAGS:
+            raise ValueError(f"FC_LIB_VARIANT token {tok!r} (known: {', '.join(VARIANT_FLAGS)})")
+        flags.append(VARIANT_FLAGS[tok])
+    # FC_HIPCC_FLAGS: extra compiler flags for experiment builds (with FC_LIB_OUT naming the output)
+    extra = os.environ.get("FC_HIPCC_FLAGS", "").split()
+    flags += extra
+    if VARIANT or extra:
+        flags.append("-DFC_VARIANT_BUILD")
+    return flags
+
+
+def source_id() -> str:
+    """SHA-256 over every source and header (name and bytes) and the compiler flags: the id the
+    library is built with (``fc_build_id()``) and the one a current library must carry."""
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        h.update(f.encode() + b"\0")
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(_flags()).encode())
+    return h.hexdigest()[:32]
+
+
+def library_id(path: str = None) -> str:
+    """The build id embedded in a built library (the ``FC_BUILD_ID=`` marker), or "" if none."""
+    path = path or LIB
+    try:
+        with open(path, "rb") as fh:
+            m = re.search(rb"FC_BUILD_ID=([0-9a-f]{32})", fh.read())
+    except OSError:
+        return ""
+    return m.group(1).decode() if m else ""
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+    """Rebuild when the library is missing or was built from other sources / flags (by content
+    hash, not file times: a snapshot copy or checkout resets mtimes)."""
+    return not os.path.exists(LIB) or library_id(LIB) != source_id()
 
 
 def _run(cmd, verbose):
@@ -49,16 +86,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     then link the shared library."""
     if not force and not _stale():
         return LIB
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
-    for tok in filter(None, VARIANT.split("_")):
-        if tok not in VARIANT_FLAGS:
-            raise ValueError(f"FC_LIB_VARIANT token {tok!r} (known: {', '.join(VARIANT_FLAGS)})")
-        flags.append(VARIANT_FLAGS[tok])
-    # FC_HIPCC_FLAGS: extra compiler flags for experiment builds (with FC_LIB_OUT naming the output)
-    extra = os.environ.get("FC_HIPCC_FLAGS", "").split()
-    flags += extra
-    if VARIANT or extra:
-        flags.append("-DFC_VARIANT_BUILD")
+    flags = _flags() + [f'-DFC_BUILD_ID="{source_id()}"']
     with tempfile.TemporaryDirectory(prefix="fc_build_") as tmp:
         objs = [os.path.join(tmp, os.path.splitext(src)[0] + ".o") for src in SOURCES]
         jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(SOURCES), os.cpu_count() or 1, 8)

@@ -184,6 +184,14 @@ extern "C" {
 
 const char *fc_last_error(void) { return g_err.c_str(); }
 
+#ifndef FC_BUILD_ID
+#define FC_BUILD_ID "unknown"
+#endif
+// the marker lets build.py read the id from the .so bytes without loading the library
+static const char kBuildIdMarker[] = "FC_BUILD_ID=" FC_BUILD_ID;
+
+const char *fc_build_id(void) { return kBuildIdMarker + 12; }
+
 uint32_t fc_build_flags(void) {
     uint32_t f = 0;
 #ifdef FC_PHASE_PROF

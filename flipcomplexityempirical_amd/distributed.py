@@ -52,9 +52,16 @@ def group_aggregate(stats: Dict[str, np.ndarray], groups: np.ndarray, n_groups: 
     return out
 
 
-def allreduce_sum(arr: np.ndarray, dist=None, device=None) -> np.ndarray:
+def _collective(dist, force: bool) -> bool:
+    """Whether to call the collective: a process group of more than one rank, or any process
+    group when ``force`` (a world-size-1 group still runs the RCCL / gloo call, so the device
+    tensor path is exercised on one GPU)."""
+    return dist is not None and dist.is_initialized() and (force or dist.get_world_size() > 1)
+
+
+def allreduce_sum(arr: np.ndarray, dist=None, device=None, force: bool = False) -> np.ndarray:
     """Sum ``arr`` over ranks (identity without a process group)."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _collective(dist, force):
         return arr
     import torch
     t = torch.as_tensor(np.ascontiguousarray(arr), device=device)
@@ -62,8 +69,8 @@ def allreduce_sum(arr: np.ndarray, dist=None, device=None) -> np.ndarray:
     return t.cpu().numpy()
 
 
-def allreduce_max(x: float, dist=None, device=None) -> float:
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+def allreduce_max(x: float, dist=None, device=None, force: bool = False) -> float:
+    if not _collective(dist, force):
         return x
     import torch
     t = torch.tensor([x], dtype=torch.float64, device=device)
@@ -140,14 +147,15 @@ def _unpack(flat: np.ndarray, layout) -> Dict[str, np.ndarray]:
     return out
 
 
-def allreduce_statistics(local: Dict[str, np.ndarray], dist=None, device=None) -> Dict[str, np.ndarray]:
+def allreduce_statistics(local: Dict[str, np.ndarray], dist=None, device=None,
+                         force: bool = False) -> Dict[str, np.ndarray]:
     """Every rank's ``local_statistics`` combined: one SUM all-reduce of the packed additive
     fields (scalars, histograms, cut_times, num_flips, part_sum; all ``[n_groups, ...]``) and
     one MAX all-reduce of last_flipped.  Every rank must pass the same set of fields with the
     same shapes (the same n_groups, even where it runs no chain of a group)."""
     flat_s, lay_s = _pack(local, ("scalars",) + SUM_ARRAYS)
     flat_m, lay_m = _pack(local, MAX_ARRAYS)
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+    if _collective(dist, force):
         import torch
         t = torch.as_tensor(flat_s, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)

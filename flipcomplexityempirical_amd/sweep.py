@@ -79,7 +79,8 @@ class Sweep:
 
     def __init__(self, graph: str = "sec11", replicas: int = 1, total_steps: int = 100000, seed: int = 0,
                  device: int = 0, series: bool = True, corrected: bool = True,
-                 configs: Optional[Sequence[SweepConfig]] = None, dist=None, dist_device=None):
+                 configs: Optional[Sequence[SweepConfig]] = None, dist=None, dist_device=None,
+                 force_collective: bool = False):
         self.graph = graph
         self.configs = list(configs) if configs is not None else sweep_configs(graph)
         if not self.configs or any(c.graph != graph for c in self.configs):
@@ -89,6 +90,7 @@ class Sweep:
         self.replicas, self.total_steps, self.seed = int(replicas), int(total_steps), int(seed)
         self.series, self.corrected = bool(series), bool(corrected)
         self.dist, self.dist_device = dist, dist_device
+        self.force_collective = bool(force_collective)  # collectives even at world size 1
         self.world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
         self.spec = G.sec11_graph() if graph == "sec11" else G.frank_graph()
@@ -199,11 +201,11 @@ class Sweep:
                       "last_flipped": np.zeros((0, n))}
         groups = self.gids % self.n_configs
         red = D.allreduce_statistics(D.local_statistics(st, groups, self.n_configs, arrays), self.dist,
-                                     self.dist_device)
+                                     self.dist_device, force=self.force_collective)
         per_chain = np.zeros((3, self.n_total), dtype=np.int64)
         if run is not None:
             per_chain[:, self.offset:self.offset + self.count] = (st["sum_wait"], st["cut"], st["nb"])
-        per_chain = D.allreduce_sum(per_chain, self.dist, self.dist_device)
+        per_chain = D.allreduce_sum(per_chain, self.dist, self.dist_device, force=self.force_collective)
         shape = (self.replicas, self.n_configs)
         red["chain_sum_wait"] = per_chain[0].reshape(shape)
         red["chain_cut"] = per_chain[1].reshape(shape)

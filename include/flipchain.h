@@ -399,6 +399,11 @@ const char *fc_last_error(void);
 #define FC_BUILD_PHASE_SYNC 0x2u   /* -DFC_PHASE_SYNC: each stamp drains outstanding memory     */
 #define FC_BUILD_VARIANT 0x4u      /* built with FC_LIB_VARIANT / FC_HIPCC_FLAGS (tools only)   */
 uint32_t fc_build_flags(void);
+/* Identity of the sources this library was compiled from: the hex SHA-256 of every source and
+ * header plus the compiler flags, passed in by the build (flipcomplexityempirical_amd/build.py).
+ * The in-tree loader rebuilds when it differs from the current sources' id (never by file
+ * times), and profiles record it so counters are matched to the kernel revision they measured. */
+const char *fc_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -547,10 +547,19 @@ class NativeRngChain(GcFaithfulChain):
     proposal, words 4-5 the 53-bit ``random_sample()`` numpy's geometric inverted for the
     state it created -- plus the initial state's wait words (``fc_run_set_initial_wait``)
     and the per-proposal trace in the device's record layout.  Every draw of this chain is a
-    proposal (it samples B itself), so tape draw i is proposal i."""
+    proposal (it samples B itself), so tape draw i is proposal i.
+
+    ``pair=True`` runs ``slow_reversible_propose`` (:117-130) instead: one
+    ``random.choice(list(pairs))`` over the (node, district) pairs of ``b_nodes`` (:151-153),
+    then ``partition.flip({node: district})``.  The pair set is the proposal's own (the inline
+    form commented at :125-126); the ``"b_nodes"`` updater stays ``b_nodes_bi`` as registered at
+    :305, so ``geom_wait`` (:148) and the driver's ``rbn`` (:369) keep counting nodes.  The node
+    tape then also carries word 3: the Lemire word that sends the state's slot bound ``wcap``
+    (its largest foreign-district count, the canonical PAIR stream's bound) to the drawn
+    district's rank among the node's foreign districts, ascending."""
 
     def __init__(self, spec, plan: Dict, *, base: float, pop_bounds, seed: int,
-                 log1mp: Optional[np.ndarray] = None, record: bool = False):
+                 log1mp: Optional[np.ndarray] = None, record: bool = False, pair: bool = False):
         import random as _random
         self.rng = _random.Random(seed)
         self.nprng = np.random.RandomState(seed & 0xFFFFFFFF)
@@ -558,7 +567,8 @@ class NativeRngChain(GcFaithfulChain):
         self.tape_words = []      # 6 u32 per proposal
         self.wait0_words = None
         self._geom_words = None   # words of the last geometric draw
-        super().__init__(spec, plan, base=base, pop_bounds=pop_bounds, seed=seed, chain_id=0, log1mp=log1mp)
+        super().__init__(spec, plan, base=base, pop_bounds=pop_bounds, seed=seed, chain_id=0, log1mp=log1mp,
+                         pair=pair)
         if record:
             self.wait0_words = self._geom_words
 
@@ -570,13 +580,25 @@ class NativeRngChain(GcFaithfulChain):
         assert x / 9007199254740992.0 == u
         return (x >> 26) << 5, (x & ((1 << 26) - 1)) << 6
 
-    def _node_word(self, v: int) -> int:
+    @staticmethod
+    def _lemire_word(v: int, N: int) -> int:
         """x0 with (x0 * N) >> 32 == v and (x0 * N) mod 2^32 >= 2^32 mod N (never rejected)."""
-        N = self.n
         x0 = (((v + 1) << 32) - 1) // N
         m = x0 * N
         assert m >> 32 == v and (m & 0xFFFFFFFF) >= (1 << 32) % N
         return x0
+
+    def _node_word(self, v: int) -> int:
+        return self._lemire_word(v, self.n)
+
+    def _slot_word(self, node, target) -> int:
+        """Word 3 of a PAIR proposal: rank of ``target`` among ``node``'s foreign districts
+        (ascending label order, as the canonical stream ranks them) under the slot bound."""
+        s = self.state
+        a = s.assignment
+        foreign = sorted({a[y] for y in self.g.neighbors(node) if a[y] != a[node]}, key=self.labels.index)
+        wcap = s["pair_slots"]
+        return self._lemire_word(foreign.index(target), wcap)
 
     def _geom(self, d, purpose):
         if self.log1mp is None:
@@ -589,8 +611,14 @@ class NativeRngChain(GcFaithfulChain):
             U = clone.random_sample()
             self._geom_words = self._u53_words(U)
         w = int(self.nprng.geometric(p, 1)[0]) - 1
+        nb = len(s["b_nodes"])
+        if float(self.log1mp[nb]) == 0.0:
+            # 1 - p rounds to 1.0 (N^k beyond 2^53 |B|, e.g. k = 8 on 3,120 nodes): numpy's
+            # inversion divides by log(1.0) = 0 and casts +inf to int64, which gives INT64_MIN;
+            # the C restatement and the device saturate at 2^62 instead (flipref.c geom_wait).
+            assert w == -(1 << 63) - 1, (p, w)
+            return 1 << 62
         if self.record:  # the replayed inversion must give numpy's own answer
-            nb = len(s["b_nodes"])
             q = math.log(1.0 - U) / float(self.log1mp[nb])
             assert int(math.ceil(q)) - 1 == w, (U, p, w)
         return w
@@ -598,13 +626,18 @@ class NativeRngChain(GcFaithfulChain):
     def step(self):
         while True:
             s = self.state
-            node = self.rng.choice(list(s["b_nodes"]))  # :143
+            if self.pair:
+                node, target = self.rng.choice(list(s["pairs"]))  # :128 over the :151-153 pairs
+            else:
+                node = self.rng.choice(list(s["b_nodes"]))  # :143
+                target = -1 * s.assignment[node]  # :145
             draw = self.stats["draws"]
             self.stats["draws"] += 1
             self.stats["proposals"] += 1
-            target = -1 * s.assignment[node]  # :145
             tid = self.labels.index(target) << 8
             words = [self._node_word(self.spec.index[node]), 0, 0, 0, 0, 0] if self.record else None
+            if self.record and self.pair:
+                words[3] = self._slot_word(node, target)
             proposal = s.flip({node: target})
             s.parent = None
             old_nbrs = [nd for nd in self.g.neighbors(node) if proposal.assignment[nd] == s.assignment[node]]

@@ -163,3 +163,33 @@ def test_group_arrays_edge_cases():
     assert D.sweep_groups(10, 3, offset=4, count=4).tolist() == [1, 2, 0, 1]
     cs = D.group_checksums({"x": s})
     assert cs["x"][1] == 0 and cs["x"][0] == D.checksums({"x": s[0]})["x"]
+
+
+def test_forced_collective_world1_gloo():
+    """``force=True`` runs the collectives at world size 1 (the path tests/test_rccl_gpu.py takes
+    over RCCL on the GPU box): identity results, through the real gloo all-reduce calls."""
+    import socket
+    import torch.distributed as dist
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        calls = []
+        real = dist.all_reduce
+        dist.all_reduce = lambda t, op=None: (calls.append(op), real(t, op=op))[1]
+        try:
+            rng = np.random.default_rng(2)
+            st = {f: rng.integers(0, 1000, 10) for f in D.AGG_FIELDS}
+            loc = D.local_statistics(st, np.arange(10) % 3, 3, {"last_flipped": rng.integers(0, 99, (10, 4))})
+            red = D.allreduce_statistics(loc, dist, force=True)
+            assert np.array_equal(red["scalars"], loc["scalars"])
+            assert np.array_equal(red["last_flipped"], loc["last_flipped"])
+            assert D.allreduce_max(2.5, dist, force=True) == 2.5
+            assert len(calls) == 3
+            D.allreduce_statistics(loc, dist)  # no force: no collective at one rank
+            assert len(calls) == 3
+        finally:
+            dist.all_reduce = real
+    finally:
+        dist.destroy_process_group()

@@ -99,6 +99,60 @@ def shape_from_events(spec, frame, a0, events, T):
     return mean, vals[-1]
 
 
+# --- C3: k = 4, the pair proposal (slow_reversible_propose, grid_chain_sec11.py:117-130) -------
+C3_STATS = ("cut", "nb", "pop0", "wait", "mean_cut", "mean_nb", "perim0", "radius0")
+C3_K, C3_PCT = 4, 0.05
+
+
+def setup_c3():
+    spec = G.sec11_graph()
+    a0 = spec.assignment_array(G.quadrant_plan(spec.nodes), list(range(C3_K)))
+    _, (lo, hi) = G.population_bounds(spec.n, C3_K, C3_PCT)
+    return spec, a0, lo, hi
+
+
+def summarize_c3(spec, finals, waits, sum_cut, sum_nb, T):
+    """The C3 fixture's statistics (tests/golden/make_native.py one_c3) from end states and tallies."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_native import c3_shape
+    out = {s: [] for s in C3_STATS}
+    for a in finals:
+        c, b, pops = G.cut_and_boundary(spec, a)
+        p0, r0 = c3_shape(spec, a)
+        for key, val in (("cut", c), ("nb", b), ("pop0", pops[0]), ("perim0", p0), ("radius0", r0)):
+            out[key].append(val)
+    out["wait"] = list(waits)
+    out["mean_cut"] = np.asarray(sum_cut, float) / (T + 1)
+    out["mean_nb"] = np.asarray(sum_nb, float) / (T + 1)
+    return {key: np.asarray(v, float) for key, v in out.items()}
+
+
+def assert_same_distribution_c3(fix, bi, got, label):
+    for s in C3_STATS:
+        ref = fix[f"b{bi}_{s}"]
+        p = ks_2samp(ref, np.asarray(got[s], float)).pvalue
+        assert p > P_MIN, (label, s, p, ref.mean(), np.mean(got[s]))
+
+
+@pytest.mark.parametrize("bi", [0, 1])
+def test_c3_canonical_oracle_matches_native_rng_pair(cref, bi):
+    """C3 under the canonical PAIR stream (C oracle) against the reference's pair proposal under
+    CPython's MT (native_rng_c3.npz): KS on cut, boundary, population and shape statistics."""
+    fix = fixture("c3")
+    T, base = int(fix["T"]), float(fix["bases"][bi])
+    spec, a0, lo, hi = setup_c3()
+    finals, waits, sc, sn = [], [], [], []
+    for c in range(400):
+        r = cref.run(spec, a0, base=base, pop_lo=lo, pop_hi=hi, seed=0xC3, chain_id=c, n_steps=T, k=C3_K,
+                     labels=list(range(C3_K)), proposal=1, log1mp=G.log1mp_table(spec.n, C3_K))
+        finals.append(r["final"])
+        waits.append(r["stats"]["wait_cur"])
+        sc.append(r["stats"]["sum_cut"])
+        sn.append(r["stats"]["sum_nb"])
+    assert_same_distribution_c3(fix, bi, summarize_c3(spec, finals, waits, sc, sn, T), "C oracle c3")
+
+
 @pytest.mark.parametrize("stream", [0, 1], ids=["node", "band"])
 @pytest.mark.parametrize("cfg,bi", CASES)
 def test_canonical_oracle_matches_native_rng(cref, cfg, bi, stream):

@@ -6,7 +6,8 @@ import pytest
 from flipcomplexityempirical_amd import _lib
 from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
 from flipcomplexityempirical_amd import graphs as G
-from tests.test_distribution import CASES, assert_same_distribution, fixture, setup, summarize
+from tests.test_distribution import (C3_K, CASES, assert_same_distribution, assert_same_distribution_c3, fixture,
+                                     setup, setup_c3, summarize, summarize_c3)
 
 pytestmark = pytest.mark.gpu
 
@@ -45,3 +46,23 @@ def test_device_matches_native_rng(gpu, cfg, bi):
                 ae[c] = ang[-1] if two[-1] else np.nan
         got["angle_mean"], got["angle_end"] = am, ae
     assert_same_distribution(fix, bi, got, f"device {cfg}")
+
+
+@pytest.mark.parametrize("bi", [0, 1])
+def test_device_c3_matches_native_rng_pair(gpu, bi):
+    """C3 at its per-GPU production shape (8192 chains; the general-k kernel with the multi-flip
+    commit, canonical Philox PAIR stream) against the reference's pair proposal under native RNG
+    (native_rng_c3.npz): KS on the end state's cut, boundary, population and shape statistics,
+    the time-averaged cut and boundary, and the geometric wait."""
+    fix = fixture("c3")
+    T, base = int(fix["T"]), float(fix["bases"][bi])
+    spec, a0, lo, hi = setup_c3()
+    C = 8192
+    run = FlipRun(FlipGraph(spec), np.stack([a0] * C),
+                  RunConfig(k=C3_K, labels=tuple(range(C3_K)), proposal=_lib.FC_PROPOSE_PAIR, seed=0xC3C3 + bi,
+                            pop_lo=lo, pop_hi=hi, base=base, diag_mask=_lib.FC_DIAG_WAIT))
+    run.steps(T)
+    st, fin = run.stats(), run.state()
+    assert int(st["steps"].min()) == T
+    got = summarize_c3(spec, fin, st["wait_cur"], st["sum_cut"], st["sum_nb"], T)
+    assert_same_distribution_c3(fix, bi, got, "device c3")

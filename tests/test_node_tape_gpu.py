@@ -12,26 +12,28 @@ from flipcomplexityempirical_amd import _lib
 from flipcomplexityempirical_amd import graphs as G
 from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
 
-from test_node_tape import FIELDS, record
+from test_node_tape import FIELDS, PAIR_CASES, record, wrap64
 
 pytestmark = pytest.mark.gpu
 
 STATS = ("steps", "proposals", "draws", "accepted", "inv_contig", "inv_pop", "sum_cut", "sum_nb", "sum_wait", "cut", "nb")
 
 
-def _replay(spec, plans, bases, pct, steps, seeds, *, lean=False, chunks=(None,)):
-    chains = [record(spec, plans[i], bases[i], pct, seeds[i], steps) for i in range(len(plans))]
+def _replay(spec, plans, bases, pct, steps, seeds, *, lean=False, chunks=(None,), k=2, tune=None):
+    chains = [record(spec, plans[i], bases[i], pct, seeds[i], steps, k=k) for i in range(len(plans))]
     tapes = [ch.node_tape() for ch in chains]
     L = max(t.size for t in tapes)
     tape = np.zeros((len(chains), L), dtype=np.uint32)
     for i, t in enumerate(tapes):
         tape[i, :t.size] = t
-    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), 2, pct)
-    inits = np.stack([spec.assignment_array(p, [-1, 1]) for p in plans])
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), k, pct)
+    labels = [-1, 1] if k == 2 else list(range(k))
+    inits = np.stack([spec.assignment_array(p, labels) for p in plans])
     n_trace = 0 if lean else len(chains)
-    cfg = RunConfig(seed=1, pop_lo=lo, pop_hi=hi, trace_chains=n_trace,
+    cfg = RunConfig(k=k, labels=tuple(labels), proposal=_lib.FC_PROPOSE_BI_SIGN if k == 2 else _lib.FC_PROPOSE_PAIR,
+                    seed=1, pop_lo=lo, pop_hi=hi, trace_chains=n_trace,
                     trace_cap=0 if lean else max(len(ch.trace) for ch in chains) + 64,
-                    diag_mask=_lib.FC_DIAG_WAIT if lean else _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST)
+                    diag_mask=_lib.FC_DIAG_WAIT if lean else _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST, tune=tune)
     run = FlipRun(FlipGraph(spec), inits, cfg, bases=np.asarray(bases, dtype=np.float64))
     run.set_tape(tape)
     run.set_initial_wait(np.asarray([ch.wait0_words for ch in chains], dtype=np.uint32))
@@ -54,7 +56,7 @@ def _compare(chains, run, lean):
                 ref = len(ch.state["cut_edges"])
             elif k == "nb":
                 ref = len(ch.state["b_nodes"])
-            assert int(st[k][c]) == int(ref), (c, k, int(st[k][c]), ref)
+            assert int(st[k][c]) == wrap64(ref), (c, k, int(st[k][c]), ref)
         assert int(st["wait_cur"][c]) == int(ch.wait), c
         assert np.array_equal(fin[c], ch.assignment_ids()), c
         if not lean:
@@ -84,6 +86,25 @@ def test_device_replays_native_rng_c1_and_frank(gpu, frank):
     _compare(chains, run, False)
     plans = [G.frank_plan(al, frank.nodes) for al in range(3)]
     chains, run = _replay(frank, plans, [0.3, 1 / 0.3, 1.0], 0.05, 1500, seeds=[11, 12, 13])
+    _compare(chains, run, False)
+
+
+@pytest.mark.parametrize("chunks", [(None,), (1, 400, None)], ids=["1launch", "3launches"])
+@pytest.mark.parametrize("name", sorted(PAIR_CASES))
+def test_device_replays_native_rng_pair(gpu, name, chunks):
+    """k > 2: the reference's pair proposal ``slow_reversible_propose`` (:117-130) under CPython's
+    MT, replayed on the general-k kernel with the multi-flip commit forced on (several
+    independent accepted flips per ring pass): every proposal (node, target district, verdict,
+    |cut|, |B|, wait), the tallies and the end state, in one launch and in three.  Four
+    recorded chains of different bases and seeds share each launch."""
+    mk, plan_of, k, base, pct, steps = PAIR_CASES[name]
+    spec = mk()
+    plan = plan_of(spec)
+    bases = [base, 1.0, 0.5, 3.0]
+    chains, run = _replay(spec, [plan] * 4, bases, pct, steps, seeds=[4100 + i for i in range(4)], k=k,
+                          chunks=chunks, tune={"multi_flip": 1})
+    name_k = run.kernel_name()
+    assert name_k.startswith("fc::flip_kernel<") and name_k.endswith((", true, 1>", ", true, 2>")), name_k
     _compare(chains, run, False)
 
 
