@@ -815,6 +815,8 @@ def main():
         "per_rank_kernel_ms": [float(x) for x in rank_rec[0]],
         "per_rank_elapsed_s": [float(x) for x in rank_rec[1]],
         "build_flags": _lib.build_flags(),
+        "build_id": _lib.build_id(),
+        "hip_runtime": _lib.hip_runtime_path(),
         "data": W.data + (" (band node stream: draws over b_nodes + neighbours)" if stream == "band" else ""),
         "config": {"workload": W.desc, "graph": args.workload, "k": W.k, "chains_per_gpu": C,
                    "chain_steps_per_launch": args.chain_steps,

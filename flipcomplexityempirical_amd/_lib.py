@@ -121,6 +121,22 @@ def build_flags() -> int:
     return int(load().fc_build_flags())
 
 
+def hip_runtime_path() -> str:
+    """The HIP runtime this process mapped (``/proc/self/maps``): /opt/rocm's when the library is
+    loaded first, torch's bundled copy when torch initialised its runtime first (same soname, so
+    the library binds to it) -- one runtime per process either way."""
+    seen = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if line.strip() else ""
+                if "libamdhip64" in p and p not in seen:
+                    seen.append(p)
+    except OSError:
+        pass
+    return ";".join(seen)
+
+
 def build_id() -> str:
     """``fc_build_id()`` of the loaded library: the content hash of the sources it was built from."""
     return load().fc_build_id().decode()

@@ -56,7 +56,17 @@ def _collective(dist, force: bool) -> bool:
     """Whether to call the collective: a process group of more than one rank, or any process
     group when ``force`` (a world-size-1 group still runs the RCCL / gloo call, so the device
     tensor path is exercised on one GPU)."""
-    return dist is not None and dist.is_initialized() and (force or dist.get_world_size() > 1)
+    if not (dist is not None and dist.is_initialized() and (force or dist.get_world_size() > 1)):
+        return False
+    if dist.get_backend() == "nccl":
+        import torch
+        if not torch.cuda.is_available():
+            # the flip-chain library was loaded before torch started its HIP runtime: the process
+            # then holds two runtimes and torch's finds no GPU.  Start torch.cuda first (bench.py
+            # _dist, sweep.main) so the library binds to the same runtime.
+            raise RuntimeError("RCCL collective requested but torch.cuda is unavailable in this process: initialise "
+                               "torch.cuda (and the process group) before loading libflipchain.so")
+    return True
 
 
 def allreduce_sum(arr: np.ndarray, dist=None, device=None, force: bool = False) -> np.ndarray:
