@@ -216,10 +216,12 @@ def resident_chains(fg, W, device: int = 0) -> int:
     return cus * max(1, min(160 * 1024 // lds, 16))
 
 
-def measured_l2(wname: str, kname: str, chains: int, chain_steps: int, kernel_ms: float):
+def measured_l2(wname: str, kname: str, chains: int, chain_steps: int, kernel_ms: float, build_id: str = ""):
     """The newest committed L1 / L2 counter summary of this workload's kernel at this launch shape
     (profiles/*_<workload>_l1l2.json, tools/gpu_cache_pmc.sh), rescaled to this run's launch time:
-    L2 requests per launch priced at a 128-B line (an upper bound), hit rates, wave-state shares."""
+    L2 requests per launch priced at a 128-B line (an upper bound), hit rates, wave-state shares.
+    The kernel name does not identify a kernel revision, so a summary counts only when it records
+    the library build id (fc_build_id) of this run; else None (stale counters are not reported)."""
     import glob as _glob
     best = None
     for fn in sorted(_glob.glob(os.path.join(ROOT, "profiles", f"*_{wname}_l1l2.json"))):
@@ -227,7 +229,8 @@ def measured_l2(wname: str, kname: str, chains: int, chain_steps: int, kernel_ms
             j = json.load(open(fn))
         except (OSError, ValueError):
             continue
-        if j.get("kernel") == kname and j.get("chains") == chains and j.get("chain_steps") == chain_steps:
+        if (j.get("kernel") == kname and j.get("chains") == chains and j.get("chain_steps") == chain_steps
+                and build_id and j.get("build_id") == build_id):
             best = (fn, j)
     if best is None:
         return None
@@ -281,26 +284,45 @@ def launch_ranks(gpus: int) -> int:
     Runs before anything touches the GPU (the parent never does); a rank that fails ends the
     others (their exact PIDs), and the first failing status is returned.  Rank 0 prints the
     line."""
+    import signal
     import subprocess
     port = int(os.environ.get("MASTER_PORT") or _free_port())
     procs = []
-    for r in range(gpus):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FC_BENCH_LAUNCHER="bench.py")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def _term(signum, frame):  # a scheduler that signals only this PID: end the ranks too
+        raise KeyboardInterrupt(f"signal {signum}")
+    old_term = signal.signal(signal.SIGTERM, _term)
     status = 0
-    live = list(procs)
-    while live:
-        time.sleep(0.2)
-        for pr in list(live):
-            rc = pr.poll()
-            if rc is None:
-                continue
-            live.remove(pr)
-            if rc != 0 and status == 0:
-                status = rc if rc > 0 else 128 - rc
-                for other in live:
-                    other.terminate()
+    try:
+        for r in range(gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FC_BENCH_LAUNCHER="bench.py")
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        live = list(procs)
+        while live:
+            time.sleep(0.2)
+            for pr in list(live):
+                rc = pr.poll()
+                if rc is None:
+                    continue
+                live.remove(pr)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    for other in live:
+                        other.terminate()
+    finally:
+        # however this loop ends (a failed rank, SIGTERM, KeyboardInterrupt), no rank outlives
+        # the launcher: terminate the live ones (their exact PIDs), then reap every child
+        for pr in procs:
+            if pr.poll() is None:
+                pr.terminate()
+        for pr in procs:
+            try:
+                pr.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                pr.kill()
+                pr.wait()
+        signal.signal(signal.SIGTERM, old_term)
     return status
 
 
@@ -803,7 +825,7 @@ def main():
         except Exception:
             traffic = None
     levels = roofline_levels(W, per_launch_props, per_launch_acc, kernel_ms, traffic)
-    l1l2 = measured_l2(args.workload, kname, C, args.chain_steps, kernel_ms)
+    l1l2 = measured_l2(args.workload, kname, C, args.chain_steps, kernel_ms, _lib.build_id())
     out = {
         "metric": METRIC if args.workload == "c2" else f"flip proposals/sec, side workload {args.workload}",
         "value": value, "unit": "proposals/s", "n_gpus": world, "steps": args.steps,

@@ -428,9 +428,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: graph too large for the wave-per-chain LDS layout");
 
     // ---- launch tuning (scheduling only; 0 = default) --------------------------------------
-    // k = 2: up to four rounds of 64 draws per batch, no further round once 32 draws of the
-    // batch hit the boundary (short-boundary chains, which set the launch time, draw 256 per
-    // batch).  C2 sweeps on one MI355X, ms per launch: before stale slots were re-evaluated
+    // k = 2 node stream: a window of up to 64 * nsub = 256 draws per batch (the four node words
+    // of one Philox call per lane), closed by the 64th boundary hit -- no round cut-off (the band
+    // stream keeps rounds of 64 with the hit_stop cut-off).  Before round 4, C2 sweeps on one MI355X, ms per launch: before stale slots were re-evaluated
     // in place, 2 rounds / 32 hits 10.7, 4 / 12 10.3 (4 / 8 10.55, 4 / 24 10.8); with the
     // re-evaluation, 4 / 12 9.33, 4 / 20..64 8.9-9.0, 2 / 32 10.3, 8 / 32..64 9.45-9.55
     {
@@ -443,6 +443,12 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         if (!recom && !(t.nsub == 1 || t.nsub == 2 || t.nsub == 4))
             return fail(FC_ERR_ARG, std::string("fc_run_create: tune_nsub must be 1, 2 or 4 for the ") +
                                         (k == 2 ? "k = 2" : "k > 2") + " kernel (got " + std::to_string(t.nsub) + ")");
+        // the round cut-off applies to the k > 2 rounds and the k = 2 band stream; the k = 2 node
+        // stream takes a window of 64 * nsub draws (four node words per lane's Philox call)
+        // closed by the 64th hit, so a cut-off there would silently change nothing
+        if (k == 2 && !recom && p->stream == FC_STREAM_NODE && p->tune_hit_stop != 0)
+            return fail(FC_ERR_ARG, "fc_run_create: tune_hit_stop has no effect on the k = 2 node stream (its batch window "
+                                    "is 64 * tune_nsub draws, closed by the 64th boundary hit); leave it 0");
         t.hit_stop = p->tune_hit_stop ? p->tune_hit_stop : 32;
         if (t.hit_stop < 1) return fail(FC_ERR_ARG, "fc_run_create: tune_hit_stop must be >= 1");
         t.par_min = p->tune_par_min ? p->tune_par_min : 3;
@@ -1019,8 +1025,15 @@ int fc_run_timings(fc_run *r, float *ms, int32_t cap, int32_t *n) {
 
 namespace {
 
+// Version of the canonical random stream a checkpoint's chains continue on:
+// 3 = round 4's k = 2 node words, four draws per purpose-3 Philox call.  A blob written under
+// another stream (magic "FCCKPT02": one call per draw) is refused, not continued on a stream
+// its trajectory never used.
+constexpr uint32_t kStreamVersion = 3;
+
 struct CkptHeader {
-    char magic[8];          // "FCCKPT02"
+    char magic[8];          // "FCCKPT03"
+    uint32_t stream_version, reserved;
     int32_t n_chains, n, n_edges, k, ring_max, proposal, npad, dgraph;
     uint32_t diag_mask;
     uint32_t chain_id_offset;
@@ -1068,7 +1081,8 @@ static std::vector<std::pair<void *, size_t>> ckpt_sections(fc_run *r) {
 
 CkptHeader ckpt_header(const fc_run *r, int64_t payload) {
     CkptHeader h{};
-    std::memcpy(h.magic, "FCCKPT02", 8);
+    std::memcpy(h.magic, "FCCKPT03", 8);
+    h.stream_version = kStreamVersion;
     h.n_chains = r->n_chains;
     h.n = r->g.n;
     h.n_edges = r->g.n_edges;
@@ -1118,7 +1132,13 @@ int fc_run_restore(fc_run *r, const void *buf, int64_t len) {
     int64_t payload = 0;
     for (const auto &sc : secs) payload += (int64_t)sc.second;
     const CkptHeader want = ckpt_header(r, payload);
+    if (std::memcmp(h.magic, "FCCKPT02", 8) == 0)
+        return fail(FC_ERR_ARG, "fc_run_restore: the checkpoint was written under an earlier random stream (FCCKPT02: one "
+                                "Philox call per k = 2 node draw); its chains cannot continue on this build's stream");
     if (std::memcmp(h.magic, want.magic, 8) != 0) return fail(FC_ERR_ARG, "fc_run_restore: not a flipchain checkpoint");
+    if (h.stream_version != kStreamVersion)
+        return fail(FC_ERR_ARG, "fc_run_restore: the checkpoint's random-stream version (" + std::to_string(h.stream_version) +
+                                    ") differs from this build's (" + std::to_string(kStreamVersion) + ")");
     if (h.n_chains != want.n_chains || h.n != want.n || h.n_edges != want.n_edges || h.k != want.k ||
         h.ring_max != want.ring_max || h.proposal != want.proposal || h.npad != want.npad || h.dgraph != want.dgraph ||
         h.diag_mask != want.diag_mask || h.ev_cap != want.ev_cap || h.payload != payload)

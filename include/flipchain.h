@@ -143,7 +143,9 @@ typedef struct fc_params {
                                    band stream: rounds of 64); k > 2 default 2 (4 when the slot
                                    bound wmax exceeds 8); anything else FC_ERR_ARG              */
     int32_t tune_hit_stop;      /* rounds of 64 (k > 2, k = 2 band stream): no further round
-                                   once a batch holds this many boundary hits (default 32)     */
+                                   once a batch holds this many boundary hits (default 32).
+                                   The k = 2 node stream has no rounds (a 64 * nsub window closed
+                                   by the 64th hit): nonzero there is FC_ERR_ARG                */
     int32_t tune_par_min;       /* k = 2: segment-parallel commit from this many acceptances on
                                    (default 3; > 64 = one event at a time)                     */
     int32_t tune_wait_queue;    /* accepted states queued for their geometric wait before one

@@ -66,9 +66,11 @@ def node_words_k2(seed: int, chain_id: int, d) -> np.ndarray:
     return np.choose((d & np.uint64(3)).astype(np.int64), w).astype(np.uint32)
 
 
-def draw_tape(seed: int, chain_id: int, n_draws: int, start: int = 0, k: int = 2) -> np.ndarray:
+def draw_tape(seed: int, chain_id: int, n_draws: int, start: int = 0, *, k: int) -> np.ndarray:
     """The canonical stream as an explicit tape: 6 u32 per draw (4 proposal words, then the
-    2 geometric-wait words of purpose 1); k = 2 takes word 0 from the four-per-call node stream."""
+    2 geometric-wait words of purpose 1); k = 2 takes word 0 from the four-per-call node stream,
+    k > 2 from the draw's own purpose-0 call.  ``k`` is required: the two streams differ in word
+    0, and a tape replayed on both sides would not show a wrong choice."""
     d = np.arange(start, start + n_draws, dtype=np.uint64)
     lo, hi = d & MASK32, d >> np.uint64(32)
     k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF

@@ -61,6 +61,13 @@ def test_checkpoint_resume_bit_exact(gpu, sec11, case):
                     bases=bases)
     with pytest.raises(ValueError):
         other.restore(blob)
+    # a blob written under another random-stream version (the round-3 magic, or a changed version
+    # field) is refused, never continued on this build's stream
+    assert blob[:8] == b"FCCKPT03"
+    with pytest.raises(ValueError, match="earlier random stream"):
+        b.restore(b"FCCKPT02" + blob[8:])
+    with pytest.raises(ValueError, match="random-stream version"):
+        b.restore(blob[:8] + (2).to_bytes(4, "little") + blob[12:])
 
 
 def test_checkpoint_resume_recom(gpu, sec11):

@@ -42,7 +42,7 @@ def test_tape_and_philox_agree(cref, sec11):
     l1 = G.log1mp_table(sec11.n, 2)
     a0 = sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1])
     _, (lo, hi) = G.population_bounds(sec11.n, 2, 0.1)
-    tape = draw_tape(9, 4, 30000)
+    tape = draw_tape(9, 4, 30000, k=2)
     r1 = cref.run(sec11, a0, base=0.8, pop_lo=lo, pop_hi=hi, seed=9, chain_id=4, n_steps=2000, log1mp=l1,
                   trace_cap=100000)
     r2 = cref.run(sec11, a0, base=0.8, pop_lo=lo, pop_hi=hi, seed=9, chain_id=4, n_steps=2000, log1mp=l1,

@@ -112,7 +112,7 @@ def test_tape_replay_matches_philox(gpu, cref, sec11):
     from oracle.flipref import draw_tape
     inits, bases = _configs(sec11, G.sec11_plan, [1.0, 10.0], 4)
     n_draws = 60000
-    tapes = np.stack([draw_tape(11, c, n_draws) for c in range(4)])
+    tapes = np.stack([draw_tape(11, c, n_draws, k=2) for c in range(4)])
     _, run_t = _run_gpu(sec11, inits, bases, steps=1000, tape=tapes)
     _, run_p = _run_gpu(sec11, inits, bases, steps=1000)
     for c in range(4):
@@ -203,16 +203,29 @@ def test_sharded_equals_unsharded(gpu, sec11):
         assert np.array_equal(part.state(), fa[off:off + cnt])
 
 
-@pytest.mark.parametrize("nsub,hit_stop,extra", [(1, 64, {}), (2, 32, {}), (4, 12, {}), (4, 32, {}), (4, 64, {}),
-                                               (4, 32, {"wait_queue": 1}), (4, 32, {"wait_queue": 3}),
-                                               (4, 32, {"par_min": 65}), (4, 32, {"par_min": 1}),
-                                               (4, 32, {"chains_per_block": 4}), (4, 32, {"deal": 1}),
-                                               (4, 32, {"prio_div": (-1, 0, 0)}),
-                                               (2, 32, {"prio_th": (-1.0, 0.0, 0.0)})])
+# (k = 2 node stream: no round cut-off -- tune_hit_stop is refused there; the band stream's
+# shapes with it are in tests/test_band_gpu.py)
+@pytest.mark.parametrize("nsub,hit_stop,extra", [(1, 0, {}), (2, 0, {}), (4, 0, {}),
+                                               (4, 0, {"wait_queue": 1}), (4, 0, {"wait_queue": 3}),
+                                               (4, 0, {"par_min": 65}), (4, 0, {"par_min": 1}),
+                                               (4, 0, {"chains_per_block": 4}), (4, 0, {"deal": 1}),
+                                               (4, 0, {"prio_div": (-1, 0, 0)}),
+                                               (2, 0, {"prio_th": (-1.0, 0.0, 0.0)})])
 @pytest.mark.parametrize("lean", [True, False])
+def test_hit_stop_refused_on_k2_node_stream(gpu, sec11):
+    """The k = 2 node stream's batch window is 64 * nsub draws closed by the 64th hit: a round
+    cut-off would change nothing, so a nonzero tune_hit_stop is an argument error there (ADVICE
+    r04), not a silent no-op."""
+    (_, _), (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 2, 0.1)
+    a0 = sec11.assignment_array(G.sec11_plan(0, sec11.nodes), [-1, 1])[None, :]
+    with pytest.raises(ValueError, match="tune_hit_stop"):
+        FlipRun(FlipGraph(sec11), a0, RunConfig(seed=1, pop_lo=lo, pop_hi=hi, tune={"hit_stop": 24}))
+    FlipRun(FlipGraph(sec11), a0, RunConfig(seed=1, pop_lo=lo, pop_hi=hi, stream="band", tune={"hit_stop": 24}))
+
+
 def test_sec11_batch_shapes(gpu, cref, sec11, nsub, hit_stop, extra, lean):
-    """Every launch-tuning field of fc_params (draw rounds per batch ``tune_nsub``, the round
-    cut-off ``tune_hit_stop``, the deferred-wait queue length, the segment-parallel threshold,
+    """Every launch-tuning field of fc_params the k = 2 node stream takes (draw rounds per batch
+    ``tune_nsub``, the deferred-wait queue length, the segment-parallel threshold,
     chains per workgroup, issue priorities, chain dealing) is a scheduling choice only: the lean instance
     (waits only) and the full instance (trace + histograms) stay bit-exact against the oracle
     under each of them (the guarantee include/flipchain.h states for fc_params.tune_*)."""

@@ -66,7 +66,9 @@ def main(tag, wl):
         "wait_inst_any_frac": c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"] if c.get("SQ_WAVE_CYCLES") else None,
         "active_inst_any_frac": c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"] if c.get("SQ_WAVE_CYCLES") else None,
     }
-    out = {"tag": tag, "workload": wl, "kernel": rf["kernel"], "kernel_ms_bench": rf["kernel_ms"],
+    # the library's content hash: bench.measured_l2 reports these counters only for the same build
+    out = {"tag": tag, "workload": wl, "kernel": rf["kernel"], "build_id": line.get("build_id"),
+           "kernel_ms_bench": rf["kernel_ms"],
            "chains": line["config"]["chains_per_gpu"], "chain_steps": line["config"]["chain_steps_per_launch"],
            "proposals_per_launch": per_launch_props, "counters_per_dispatch": c, "dispatches": n,
            "measured": meas, "levels": lv,
