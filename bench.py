@@ -200,7 +200,7 @@ LDS_GRANULE = 1280  # measured: a workgroup's LDS is allocated in 1280 B steps (
                    # 2048 B fits the first, not the second; 1280 B = 160 KiB / 128 fits both)
 
 
-def resident_chains(fg, W, device: int = 0) -> int:
+def resident_chains(fg, W, device: int = 0, flags: int = 0, tune=None) -> int:
     """Chains one GPU holds at once for workload W: CUs x min(LDS / chain LDS, 16 waves), the
     chain's LDS rounded up to the allocation granule."""
     import torch
@@ -208,7 +208,7 @@ def resident_chains(fg, W, device: int = 0) -> int:
     from flipcomplexityempirical_amd.engine import FlipRun, RunConfig
     _, (lo, hi) = G.population_bounds(int(W.spec.pop.sum()), W.k, W.pct)
     probe = FlipRun(fg, W.init_of(0)[None, :], RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal,
-                                                         pop_lo=lo, pop_hi=hi, device=device))
+                                                         pop_lo=lo, pop_hi=hi, device=device, flags=flags, tune=tune))
     lds = probe.chain_lds_bytes()
     probe.close()
     cus = torch.cuda.get_device_properties(device).multi_processor_count if torch.cuda.is_available() else 256
@@ -517,6 +517,10 @@ def main():
     ap.add_argument("--tune", default="",
                     help="launch tuning, e.g. nsub=2,hit_stop=24,prio_div=2:5:10 (fc_params.tune_*; "
                          "scheduling only)")
+    ap.add_argument("--force-bfs", action="store_true",
+                    help="FC_FLAG_FORCE_BFS: every proposal the ring rule does not prove valid goes to the device "
+                         "search instead of the district-graph / planar rules (side lines only; with "
+                         "--tune search_waves=4 the workgroup-cooperative search, BASELINE config 5)")
     ap.add_argument("--allow-variant", action="store_true",
                     help="load a profiling / experiment library (FC_LIB_PATH, FC_LIB_VARIANT): A/B tools only; "
                          "the line records fc_build_flags")
@@ -541,6 +545,7 @@ def main():
     from flipcomplexityempirical_amd import _lib
 
     tune = parse_tune(args.tune) or None
+    run_flags = _lib.FC_FLAG_FORCE_BFS if args.force_bfs else 0
     W = Workload(args.workload)
     stream = "node" if args.stream == "auto" else args.stream
     spec = W.spec
@@ -550,14 +555,14 @@ def main():
     if not args.chains and W.name in ("c4", "c5"):
         # large graphs: one chain per workgroup, LDS-bound residency; size the launch to one
         # wave of resident chains (a second, partial wave would double the launch time)
-        C = resident_chains(fg, W, local_rank)
+        C = resident_chains(fg, W, local_rank, flags=run_flags, tune=tune)
     off, cnt = D.shard(C * world, world, rank)          # weak scaling: C chains per GPU
     gids = np.arange(off, off + cnt)
     inits = np.stack([W.init_of(int(g)) for g in gids])
     bases = np.asarray([W.base_of(int(g)) for g in gids])
     _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), W.k, W.pct)
     cfg = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
-                    chain_id_offset=int(off), device=local_rank, tune=tune, stream=stream)
+                    chain_id_offset=int(off), device=local_rank, tune=tune, stream=stream, flags=run_flags)
     run = FlipRun(fg, inits, cfg, bases=bases)
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
@@ -612,7 +617,7 @@ def main():
         run.close()
         rn = FlipRun(fg, inits, RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed,
                                           pop_lo=lo, pop_hi=hi, chain_id_offset=int(off), device=local_rank,
-                                          tune=tune, stream="node"), bases=bases)
+                                          tune=tune, stream="node", flags=run_flags), bases=bases)
         rn.steps(args.chain_steps)
         rn.sync()
         if dist is not None:
@@ -665,6 +670,7 @@ def main():
             hit = (int(np.ceil(1.1 * cut0)), 10 ** 9)
         cfg_f = RunConfig(k=W.k, labels=tuple(W.labels), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi,
                           chain_id_offset=int(off), device=local_rank, diag_mask=full, tune=tune, stream=stream,
+                          flags=run_flags,
                           event_cap=(n_full * args.chain_steps + 1 if c4diag else args.chain_steps + 1 if series else 0),
                           hit_lo=hit[0], hit_hi=hit[1])
         lags = [1 << i for i in range(17)]
@@ -848,6 +854,10 @@ def main():
         "accept_per_proposal": acc / props if props else None,
         "draws_per_proposal": float(agg[:, D.AGG_FIELDS.index("draws")].sum()) / props if props else None,
         "bfs_per_proposal": float((s1["bfs_calls"] - s0["bfs_calls"]).sum()) * world / props if props else None,
+        "bfs_levels_per_search": (float((s1["bfs_levels"] - s0["bfs_levels"]).sum()) /
+                                  float((s1["bfs_calls"] - s0["bfs_calls"]).sum()))
+        if float((s1["bfs_calls"] - s0["bfs_calls"]).sum()) > 0 else None,
+        "force_bfs": bool(args.force_bfs),
         "roofline": {"bound": levels["bound"], "achieved": levels[levels["bound"]]["achieved"],
                      "peak": levels[levels["bound"]]["peak"], "unit": "GB/s",
                      "frac": levels[levels["bound"]]["frac"], "traffic": traffic,

@@ -44,6 +44,10 @@ struct fc_run {
     int32_t *d_labels = nullptr;
     int64_t *d_cut_hist = nullptr, *d_nb_hist = nullptr;
     int64_t *d_edge_acc = nullptr;
+    // k = 2 full diagnostics: the per-chain tally log (KParams tl_*), grown by fc_run_steps
+    uint32_t *d_tl = nullptr;
+    int64_t *d_tl_len = nullptr, *d_tl_t0 = nullptr;
+    int64_t tl_cap = 0;
     int64_t *d_num_flips = nullptr, *d_part_sum = nullptr, *d_last_flipped = nullptr;
     int64_t *d_flip_count = nullptr, *d_occ_acc = nullptr, *d_last_accept = nullptr;  // FC_DIAG_FLIPS_EXACT
     int32_t *d_popk = nullptr;
@@ -73,6 +77,8 @@ struct fc_run {
     // the frame tables (re-uploaded only when the frame changes), per-chain lengths / window
     // starts / counts / offsets, and the (t, slope, angle) outputs, grown on demand
     uint64_t fc_frame_hash = 0;
+    int32_t fc_rows = 0;  // rows of d_fc_tog
+    int64_t *d_fc_wcnt = nullptr;  // change points per chain and frame-series wave
     int32_t *d_fc_fuv = nullptr, *d_fc_tidx = nullptr;
     uint64_t *d_fc_tog = nullptr;
     double *d_fc_mid = nullptr;
@@ -121,9 +127,9 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_nfh, r->d_sbits, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh,
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_nfh, r->d_sbits, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh, r->d_tl, r->d_tl_len, r->d_tl_t0,
                     r->d_fs_out, r->d_fs_cnt, r->d_fc_fuv, r->d_fc_tidx, r->d_fc_tog, r->d_fc_mid, r->d_fc_len,
-                    r->d_fc_t0, r->d_fc_cnt, r->d_fc_off, r->d_fc_t, r->d_fc_sa};
+                    r->d_fc_t0, r->d_fc_cnt, r->d_fc_off, r->d_fc_t, r->d_fc_sa, r->d_fc_wcnt};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -382,9 +388,10 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     if (recom)   // fc_recom.hip: best / spop, tree slots, component / levels, order, parent, a
         r->chain_lds_bytes = fc::recom_lds_bytes(n);
     else if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, 3 BFS bitmaps, slots, commit marks (2 npad + 16),
-                      // wait / tally queue (24 B per entry), launch start time, pace, first queued yield (24)
-                      // (sec11: 10,016 B, so 16 chains still fill a CU's 160 KB)
-        r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16 + fc::kWaitQ * 24 + 24 +
+                      // wait / tally queue (24 B per entry), launch start time, pace, first queued yield,
+                      // tally-log length, launch's first yield (40) (sec11: 10,032 B, so 16 chains still
+                      // fill a CU's 160 KB at the 1280-B allocation granule)
+        r->chain_lds_bytes = 4 * r->npad + (2 * R + 2) * 8 + 24 * r->words + 5 * 64 * 4 + 16 + fc::kWaitQ * 24 + 40 +
                              (p->stream == FC_STREAM_BAND ? 8 * r->words : 0);  // the band bitmap (sec11: 200 B)
     // k > 2: with every node's ring exact (all bounded faces triangles / quadrilaterals, so the
     // rings list every face-adjacent cell) contiguity is decided by the district-graph rule
@@ -955,8 +962,48 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
         k.order = r->d_order;
         k.ctime = r->d_ctime;
     }
-    for (int64_t done = 0; done < n_steps; done += kChunk) {
-        k.n_steps = std::min(kChunk, n_steps - done);
+    // k = 2 full diagnostics: the tally log (16 B per entry), sized for this call's launches (a
+    // state's entries: one per accepted flip, plus a start-state entry per batch right after a
+    // queue flush -- n_steps + n_steps / 8 + 256 per chain covers what the reference's sweeps
+    // produce; a chain whose log fills applies the rest of its launch's tallies itself) within a
+    // tenth of the device's free memory; launches of at most 2^23 steps (an entry holds t - t0
+    // in 24 bits)
+    k.tl = nullptr;
+    k.tl_t0 = k.tl_len = nullptr;
+    k.tl_cap = 0;
+    int64_t chunk = kChunk;
+    if (r->p.k == 2 && (r->p.diag_mask & (FC_DIAG_HIST | FC_DIAG_FLIPS | FC_DIAG_FLIPS_EXACT | FC_DIAG_EDGES)) &&
+        r->g.n < 65535 && r->g.n_edges < (1 << 24)) {
+        chunk = int64_t(1) << 23;
+        const int64_t steps1 = std::min(chunk, n_steps);
+        int64_t want = steps1 + steps1 / 8 + 256;
+        if (want > r->tl_cap) {
+            size_t free_b = 0, total_b = 0;
+            HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+            const int64_t per_chain = (int64_t)((free_b / 10) / ((size_t)r->n_chains * 16));
+            want = std::min(want, std::max<int64_t>(per_chain, 0));
+            if (want > r->tl_cap) {
+                HIP_TRY(hipStreamSynchronize(s));
+                if (r->d_tl) { HIP_TRY(hipFree(r->d_tl)); r->d_tl = nullptr; }
+                r->tl_cap = 0;
+                if (int rc = dalloc(&r->d_tl, (size_t)r->n_chains * (size_t)want * 4)) return rc;
+                r->tl_cap = want;
+            }
+        }
+        if (!r->d_tl_len) {
+            if (int rc = dalloc(&r->d_tl_len, (size_t)r->n_chains)) return rc;
+            if (int rc = dalloc(&r->d_tl_t0, (size_t)r->n_chains)) return rc;
+            HIP_TRY(hipMemsetAsync(r->d_tl_len, 0, (size_t)r->n_chains * 8, s));
+        }
+        if (r->tl_cap > 0) {
+            k.tl = r->d_tl;
+            k.tl_t0 = r->d_tl_t0;
+            k.tl_len = r->d_tl_len;
+            k.tl_cap = r->tl_cap;
+        }
+    }
+    for (int64_t done = 0; done < n_steps; done += chunk) {
+        k.n_steps = std::min(chunk, n_steps - done);
         if (max_draws <= 0) k.max_draws = 65536 * k.n_steps;
         if (k.order) {  // this launch's deal: chains by the last one's durations (first: by |B|)
             const int e = fc::launch_deal_order(r->d_ctime, r->d_sc, k.n, r->n_chains, r->deal_timed ? 1 : 0,
@@ -971,6 +1018,10 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
         const int e = r->p.k == 2 ? fc::launch_flip2(k, r->g.ring_max, s, r->kname, sizeof r->kname)
                                     : fc::launch_flip_k2(k, r->g.ring_max, s, r->kname, sizeof r->kname);
         if (e != 0) return fail(FC_ERR_HIP, std::string("flip kernel launch: ") + hipGetErrorString((hipError_t)e));
+        if (k.tl_len) {  // the launch's logged tallies, applied and the logs emptied
+            const int er = fc::launch_tally_reduce(k, r->g.ring_max, s);
+            if (er != 0) return fail(FC_ERR_HIP, std::string("tally reduce launch: ") + hipGetErrorString((hipError_t)er));
+        }
     }
     HIP_TRY(hipEventRecord(evp.second, s));
 #ifdef FC_PHASE_PROF
@@ -1470,7 +1521,8 @@ int fc_run_frame_series(fc_run *r, int32_t c0, int32_t nc, int32_t n_frame, cons
         HIP_TRY(hipMemcpy(d_tidx, tog_idx.data(), (size_t)n * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(d_len, ev_len.data(), ev_len.size() * 8, hipMemcpyHostToDevice));
         int e = fc::launch_frame_series(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, d_len, c0, nc, n_frame, d_fuv,
-                                        d_fuv + n_frame, d_mid, cx, cy, d_tidx, d_tog, cap, d_out, d_out + outn,
+                                        d_fuv + n_frame, d_mid, cx, cy, d_tidx, d_tog, (int32_t)(tog.size() / 4), n,
+                                        cap, d_out, d_out + outn,
                                         d_cnt, r->stream);
         if (e) return fail(FC_ERR_HIP, std::string("frame series: ") + hipGetErrorString((hipError_t)e));
         HIP_TRY(hipStreamSynchronize(r->stream));
@@ -1539,6 +1591,7 @@ int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_fra
         }
         HIP_TRY(hipMemcpy(r->d_fc_tidx, tog_idx.data(), (size_t)n * 4, hipMemcpyHostToDevice));
         r->fc_frame_hash = h;
+        r->fc_rows = (int32_t)(tog.size() / 4);
     }
     if (!r->d_fc_len) {
         const size_t C = (size_t)r->n_chains;
@@ -1546,6 +1599,7 @@ int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_fra
         if ((q = dalloc(&r->d_fc_t0, C))) return q;
         if ((q = dalloc(&r->d_fc_cnt, C))) return q;
         if ((q = dalloc(&r->d_fc_off, C))) return q;
+        if ((q = dalloc(&r->d_fc_wcnt, C * fc::kFrameWaves))) return q;
     }
     std::vector<fc::ChainScalars> sc(nc);
     HIP_TRY(hipMemcpy(sc.data(), r->d_sc + c0, sc.size() * sizeof(sc[0]), hipMemcpyDeviceToHost));
@@ -1563,8 +1617,8 @@ int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_fra
     int32_t *const d_fuv = r->d_fc_fuv;
     // pass 1: change points per chain -> offsets
     int e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, r->d_fc_len, c0, nc, n_frame, d_fuv,
-                                     d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->d_fc_t0,
-                                     r->d_fc_cnt, nullptr, nullptr, nullptr, nullptr, r->stream);
+                                     d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->fc_rows, n,
+                                     r->d_fc_t0, r->d_fc_cnt, nullptr, nullptr, nullptr, nullptr, r->d_fc_wcnt, r->stream);
     if (e) return fail(FC_ERR_HIP, std::string("frame changes (count): ") + hipGetErrorString((hipError_t)e));
     std::vector<int64_t> cnt(nc);
     HIP_TRY(hipMemcpyAsync(cnt.data(), r->d_fc_cnt, (size_t)nc * 8, hipMemcpyDeviceToHost, r->stream));
@@ -1590,8 +1644,8 @@ int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_fra
     HIP_TRY(hipMemcpyAsync(r->d_fc_off, offsets, (size_t)nc * 8, hipMemcpyHostToDevice, r->stream));
     double *const d_sl = r->d_fc_sa, *const d_an = r->d_fc_sa + r->fc_cap;
     e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, r->d_fc_len, c0, nc, n_frame, d_fuv,
-                                 d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->d_fc_t0, r->d_fc_cnt,
-                                 r->d_fc_off, r->d_fc_t, d_sl, d_an, r->stream);
+                                 d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->fc_rows, n,
+                                 r->d_fc_t0, r->d_fc_cnt, r->d_fc_off, r->d_fc_t, d_sl, d_an, r->d_fc_wcnt, r->stream);
     if (e) return fail(FC_ERR_HIP, std::string("frame changes (write): ") + hipGetErrorString((hipError_t)e));
     HIP_TRY(hipMemcpyAsync(t, r->d_fc_t, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
     HIP_TRY(hipMemcpyAsync(slope, d_sl, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));

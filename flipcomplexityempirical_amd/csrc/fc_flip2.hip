@@ -50,6 +50,239 @@ using namespace dev;
 #ifndef FC_PRIO_EVERY_LOG2
 #define FC_PRIO_EVERY_LOG2 4  // profiles/r04p_prio_period_ab.txt: 55.0 ms against 55.4 every 4 batches, 56.3 every batch
 #endif
+// The per-yield tallies of the reference's loop body (grid_chain_sec11.py:367-400) for one
+// accepted state and its run (kind 0: a flushed queue entry -- yield t of the flip, `run` yields,
+// node u | old-district ring bits << 16, |cut| | target << 31, |B|) or for the yields a batch's
+// start state adds right after a flush (kind 1: yields steps0 + 1 .. steps0 + r0 of the state
+// the last flip created; node last_flip | its district << 16, 0xffff: none).  Every update
+// commutes (sums and maxima), so where and in which order they are applied leaves the results
+// bit-identical: inside the flip kernel (a full log) or by tally_reduce after the launch.
+template <int RMAX>
+__device__ __forceinline__ void tally_apply(const KParams &p, int c, int64_t t, int run, uint32_t qv, uint32_t qc,
+                                            uint32_t nbk, int64_t lab0, int64_t lab1) {
+    const int n = p.n;
+    const int cq = (int)(qc & 0x7fffffffu), nbq = (int)(nbk & 0x7fffffffu);
+    if (p.diag & FC_DIAG_HIST) {
+        atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cq], (unsigned long long)run);
+        atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nbq], (unsigned long long)run);
+    }
+    const int u = (int)(qv & 0xffffu);
+    if (nbk >> 31) {  // kind 1: the start state's further yields (the per-batch form in flip2_kernel)
+        if ((p.diag & FC_DIAG_FLIPS) && u != 0xffff) {
+            const size_t o = (size_t)c * n + u;
+            atomicMax((unsigned long long *)(p.last_flipped + o), (unsigned long long)(t + run));
+            atomicAdd((unsigned long long *)(p.part_sum + o), (unsigned long long)(((qv >> 16) & 1u ? lab0 - lab1 : lab1 - lab0) * run));
+            atomicAdd((unsigned long long *)(p.num_flips + o), (unsigned long long)run);
+        }
+        return;
+    }
+    const int tg = (int)(qc >> 31);
+    const int64_t lab_t = tg ? lab1 : lab0, lab_o = tg ? lab0 : lab1;
+    const uint32_t up = qv >> 16;  // neighbours in the old district: their edges turn cut
+    if (p.diag & FC_DIAG_FLIPS) {  // the run's share (fc_run_read_flips closes the last run)
+        const size_t o = (size_t)c * n + u;
+        const int64_t t_last = t + run - 1;
+        atomicMax((unsigned long long *)(p.last_flipped + o), (unsigned long long)t_last);
+        atomicAdd((unsigned long long *)(p.part_sum + o), (unsigned long long)((lab_o - lab_t) * t_last));
+        atomicAdd((unsigned long long *)(p.num_flips + o), (unsigned long long)run);
+    }
+    if (p.diag & FC_DIAG_FLIPS_EXACT) {
+        const size_t o = (size_t)c * n + u;
+        atomicAdd((unsigned long long *)(p.flip_count + o), 1ull);
+        atomicAdd((unsigned long long *)(p.occ_acc + o), (unsigned long long)(-(lab_t - lab_o) * t));
+        atomicMax((unsigned long long *)(p.last_accept + o), (unsigned long long)t);
+    }
+    if (p.diag & FC_DIAG_EDGES) {
+        const int4 *er = (const int4 *)(p.ring_eid + (size_t)u * RMAX);
+        int eid[RMAX];
+#pragma unroll
+        for (int j = 0; j < RMAX / 4; ++j) {
+            const int4 e4 = er[j];
+            eid[4 * j] = e4.x;
+            eid[4 * j + 1] = e4.y;
+            eid[4 * j + 2] = e4.z;
+            eid[4 * j + 3] = e4.w;
+        }
+        int64_t *ea = p.edge_acc + (size_t)c * p.n_edges;
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i)
+            if (eid[i] >= 0) atomicAdd((unsigned long long *)(ea + eid[i]), (unsigned long long)(((up >> i) & 1u) ? -t : t));
+    }
+}
+
+// One tally-log entry in 16 B (one coalesced store per lane): dt = t - t0 (< 2^24: launches
+// with the log are at most 2^23 steps), run (< 2^24), |B| (< 2^16), node | ring bits << 16,
+// |cut| (< 2^24), target, kind (0: a queue entry, 1: a start state's further yields).
+__device__ __forceinline__ uint4 tally_pack(int64_t dt, int run, uint32_t qv, uint32_t qc, uint32_t nbk) {
+    const uint32_t r = (uint32_t)run, kind = nbk >> 31;
+    return make_uint4(((uint32_t)dt & 0xffffffu) | (r << 24), (r >> 8) | ((nbk & 0xffffu) << 16), qv,
+                      (qc & 0xffffffu) | ((qc >> 31) << 24) | (kind << 25));
+}
+
+// Apply every chain's tally log and reset it: one workgroup per chain, after the flip kernel on
+// the same stream, so the chain's serial stream never waits on these updates.  Each pass keeps
+// the arrays of its mask (TR_* bits) privatised in LDS -- zeroed, every entry of the log applied
+// with LDS atomics, then added (maxed) into the chain's global rows -- and applies the arrays of
+// `gmask` with global atomics (those too large for any pass).  Global atomics from a separate
+// kernel, for all arrays, took 62 ms per C2 launch: the chains' rows do not stay in L2.
+enum : uint32_t { TR_CUT = 1, TR_NB = 2, TR_EDGE = 4, TR_NF = 8, TR_PS = 16, TR_LF = 32, TR_FC = 64, TR_OCC = 128, TR_LA = 256 };
+constexpr int kTrArrays = 9;
+
+__device__ __forceinline__ int64_t tr_len(const KParams &p, int a) {  // entries of array a per chain
+    return a == 0 ? (int64_t)p.n_edges + 1 : a == 1 ? (int64_t)p.n + 1 : a == 2 ? (int64_t)p.n_edges : (int64_t)p.n;
+}
+__device__ __forceinline__ int64_t *tr_row(const KParams &p, int a, int c) {  // chain c's global row
+    int64_t *b = a == 0 ? p.cut_hist : a == 1 ? p.nb_hist : a == 2 ? p.edge_acc : a == 3 ? p.num_flips
+               : a == 4 ? p.part_sum : a == 5 ? p.last_flipped : a == 6 ? p.flip_count : a == 7 ? p.occ_acc : p.last_accept;
+    return b + (size_t)c * (size_t)tr_len(p, a);
+}
+
+template <int RMAX>
+__global__ __launch_bounds__(1024) void tally_reduce_kernel(KParams p, uint32_t lmask, uint32_t gmask, int last) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned long long *acc = (unsigned long long *)smem;
+    const int c = (int)blockIdx.x;
+    const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+    const int64_t len = p.tl_len[c];
+    const int64_t lab0 = p.labels[0], lab1 = p.labels[1];
+    // LDS offsets (in entries) of the arrays of this pass, in TR order
+    int64_t off[kTrArrays];
+    int64_t tot = 0;
+#pragma unroll
+    for (int a = 0; a < kTrArrays; ++a) {
+        off[a] = tot;
+        if ((lmask >> a) & 1u) tot += tr_len(p, a);
+    }
+    for (int64_t i = tid; i < tot; i += nt) acc[i] = 0ull;
+    __syncthreads();
+    const uint4 *lg = (const uint4 *)p.tl + (size_t)c * (size_t)p.tl_cap;
+    const int64_t t0 = p.tl_t0[c];
+    // one update: LDS when the array is in this pass, global when it is in gmask
+    auto add = [&](int a, int64_t i, int64_t v) {
+        if ((lmask >> a) & 1u) atomicAdd(acc + off[a] + i, (unsigned long long)v);
+        else if ((gmask >> a) & 1u) atomicAdd((unsigned long long *)(tr_row(p, a, c) + i), (unsigned long long)v);
+    };
+    auto mx = [&](int a, int64_t i, int64_t v) {
+        if ((lmask >> a) & 1u) atomicMax(acc + off[a] + i, (unsigned long long)v);
+        else if ((gmask >> a) & 1u) atomicMax((unsigned long long *)(tr_row(p, a, c) + i), (unsigned long long)v);
+    };
+    const uint32_t want = lmask | gmask;
+    for (int64_t i = tid; i < len; i += nt) {
+        const uint4 e = lg[i];  // (tally_pack)
+        const int64_t t = t0 + (int64_t)(e.x & 0xffffffu);
+        const int run = (int)((e.x >> 24) | ((e.y & 0xffffu) << 8));
+        const uint32_t qv = e.z, qc = (e.w & 0xffffffu) | (((e.w >> 24) & 1u) << 31);
+        const int u = (int)(qv & 0xffffu);
+        if (want & TR_CUT) add(0, (int64_t)(qc & 0x7fffffffu), run);
+        if (want & TR_NB) add(1, (int64_t)(e.y >> 16), run);
+        if ((e.w >> 25) & 1u) {  // kind 1 (tally_apply)
+            if (u != 0xffff) {
+                if (want & TR_LF) mx(5, u, t + run);
+                if (want & TR_PS) add(4, u, ((qv >> 16) & 1u ? lab0 - lab1 : lab1 - lab0) * run);
+                if (want & TR_NF) add(3, u, run);
+            }
+            continue;
+        }
+        const int tg = (int)(qc >> 31);
+        const int64_t lab_t = tg ? lab1 : lab0, lab_o = tg ? lab0 : lab1;
+        const int64_t t_last = t + run - 1;
+        if (want & TR_LF) mx(5, u, t_last);
+        if (want & TR_PS) add(4, u, (lab_o - lab_t) * t_last);
+        if (want & TR_NF) add(3, u, run);
+        if (want & TR_FC) add(6, u, 1);
+        if (want & TR_OCC) add(7, u, -(lab_t - lab_o) * t);
+        if (want & TR_LA) mx(8, u, t);
+        if (want & TR_EDGE) {
+            const uint32_t up = qv >> 16;
+            const int4 *er = (const int4 *)(p.ring_eid + (size_t)u * RMAX);
+#pragma unroll
+            for (int j = 0; j < RMAX / 4; ++j) {
+                const int4 e4 = er[j];
+                const int ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (ev[q] >= 0) add(2, ev[q], ((up >> (4 * j + q)) & 1u) ? -t : t);
+            }
+        }
+    }
+    __syncthreads();
+    // the pass's sums (maxima) into the chain's rows: one workgroup per chain, so no atomics
+#pragma unroll
+    for (int a = 0; a < kTrArrays; ++a) {
+        if (!((lmask >> a) & 1u)) continue;
+        int64_t *row = tr_row(p, a, c);
+        const int64_t L = tr_len(p, a);
+        const bool is_max = a == 5 || a == 8;
+        for (int64_t i = tid; i < L; i += nt) {
+            const int64_t v = (int64_t)acc[off[a] + i];
+            if (is_max) {
+                if (v > row[i]) row[i] = v;
+            } else if (v) {
+                row[i] += v;
+            }
+        }
+    }
+    if (last) {
+        __syncthreads();
+        if (tid == 0) p.tl_len[c] = 0;
+    }
+}
+
+int launch_tally_reduce(const KParams &p, int ring_max, void *stream) {
+    if (!p.tl_len || p.n_chains <= 0) return (int)hipSuccess;
+    // the arrays this run keeps, their per-chain bytes, packed greedily into passes of at most
+    // 160 KiB of LDS (sec11 with every tally: one pass of 139 KiB, one 1024-thread workgroup per
+    // CU: the log is read once); an array above 160 KiB goes to global atomics
+    uint32_t have = 0;
+    if (p.diag & FC_DIAG_HIST) have |= TR_CUT | TR_NB;
+    if (p.diag & FC_DIAG_EDGES) have |= TR_EDGE;
+    if (p.diag & FC_DIAG_FLIPS) have |= TR_NF | TR_PS | TR_LF;
+    if (p.diag & FC_DIAG_FLIPS_EXACT) have |= TR_FC | TR_OCC | TR_LA;
+    auto bytes = [&](int a) -> size_t {
+        return 8 * (size_t)(a == 0 ? p.n_edges + 1 : a == 1 ? p.n + 1 : a == 2 ? p.n_edges : p.n);
+    };
+    constexpr size_t kPass = 160 * 1024, kMaxLds = 160 * 1024;
+    std::vector<std::pair<uint32_t, size_t>> passes;
+    uint32_t gmask = 0;
+    for (int a = 0; a < kTrArrays; ++a) {
+        if (!((have >> a) & 1u)) continue;
+        const size_t b = bytes(a);
+        if (b > kMaxLds) {
+            gmask |= 1u << a;
+            continue;
+        }
+        bool put = false;
+        for (auto &ps : passes)
+            if (ps.second + b <= std::max(kPass, b)) {
+                ps.first |= 1u << a;
+                ps.second += b;
+                put = true;
+                break;
+            }
+        if (!put) passes.emplace_back(1u << a, b);
+    }
+    if (passes.empty()) passes.emplace_back(0u, 0);
+    for (size_t i = 0; i < passes.size(); ++i) {
+        const size_t lds = passes[i].second;
+        const uint32_t g = i == 0 ? gmask : 0u;
+        const int last = i + 1 == passes.size() ? 1 : 0;
+        if (ring_max <= 8) {
+            if (lds > 65536)
+                (void)hipFuncSetAttribute((const void *)tally_reduce_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(tally_reduce_kernel<8>, dim3(p.n_chains), dim3(1024), lds, (hipStream_t)stream, p,
+                               passes[i].first, g, last);
+        } else {
+            if (lds > 65536)
+                (void)hipFuncSetAttribute((const void *)tally_reduce_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(tally_reduce_kernel<16>, dim3(p.n_chains), dim3(1024), lds, (hipStream_t)stream, p,
+                               passes[i].first, g, last);
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    return (int)hipSuccess;
+}
+
 template <int RMAX, int NSUB, bool FULL, bool SEARCH, bool XTRA, bool BAND>
 __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams p) {
     static_assert(FULL || !XTRA, "XTRA is a FULL instance");
@@ -88,10 +321,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     // FULL: the per-flip tallies of a queued state, applied by the same pass (tally_flush):
     // node | old-district neighbours (ring bits) << 16, |cut| | target district << 31
     uint32_t *q_v = q_run + kWaitQ, *q_c = q_v + kWaitQ;
-    // [3]: launch start time, previous launch's pace (read back, not held), yield of the first
-    // queued state
+    // [5]: launch start time, previous launch's pace (read back, not held), yield of the first
+    // queued state, FULL: tally-log entries written this launch, the launch's first yield
     uint64_t *misc = (uint64_t *)(q_c + kWaitQ);
-    uint64_t *const sb = misc + 3;  // BAND: [words] the band S (bit u: node u in S)
+    uint64_t *const sb = misc + 5;  // BAND: [words] the band S (bit u: node u in S)
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
 
     // ---- load the chain into LDS -------------------------------------------------------
@@ -207,60 +440,32 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             const int64_t t = (int64_t)misc[2] + (int64_t)(wave_scan_incl(run) - run);  // yield of the flip
             const uint32_t qv = in ? q_v[lane] : 0u, qc = in ? q_c[lane] : 0u;
             const int nbq = in ? (int)q_nb[lane] : 0;
-            const int u = (int)(qv & 0xffffu), cq = (int)(qc & 0x7fffffffu), tg = (int)(qc >> 31);
-            const uint32_t up = qv >> 16;  // neighbours in the old district: their edges turn cut
-            // district labels: uniform loads (scalar), not per-lane gathers that would wait
-            // behind the atomics
-            const int64_t lab0 = p.labels[0], lab1 = p.labels[1];
-            const int64_t lab_t = tg ? lab1 : lab0, lab_o = tg ? lab0 : lab1;
-            int eid[RMAX];
-            if (in && (p.diag & FC_DIAG_EDGES)) {
-                const int4 *er = (const int4 *)(p.ring_eid + (size_t)u * RMAX);
-#pragma unroll
-                for (int j = 0; j < RMAX / 4; ++j) {
-                    const int4 e4 = er[j];
-                    eid[4 * j] = e4.x;
-                    eid[4 * j + 1] = e4.y;
-                    eid[4 * j + 2] = e4.z;
-                    eid[4 * j + 3] = e4.w;
+            if (in && (p.diag & FC_DIAG_SERIES)) {
+                const int64_t idx = ev_len + lane;
+                if (idx < p.ev_cap) {
+                    fc_event ev;
+                    ev.t = t;
+                    ev.v = (uint16_t)(qv & 0xffffu);
+                    ev.cut = (uint16_t)(qc & 0x7fffffffu);
+                    ev.nb = (uint16_t)nbq;
+                    ev.target = (uint8_t)(qc >> 31);
+                    ev.reserved = 0;
+                    p.events[(size_t)c * p.ev_cap + idx] = ev;
                 }
             }
-            if (in) {
-                if (p.diag & FC_DIAG_SERIES) {
-                    const int64_t idx = ev_len + lane;
-                    if (idx < p.ev_cap) {
-                        fc_event ev;
-                        ev.t = t;
-                        ev.v = (uint16_t)u;
-                        ev.cut = (uint16_t)cq;
-                        ev.nb = (uint16_t)nbq;
-                        ev.target = (uint8_t)tg;
-                        ev.reserved = 0;
-                        p.events[(size_t)c * p.ev_cap + idx] = ev;
-                    }
-                }
-                if (p.diag & FC_DIAG_HIST) {
-                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cq], (unsigned long long)run);
-                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nbq], (unsigned long long)run);
-                }
-                if (p.diag & FC_DIAG_FLIPS) {  // the run's share, as in the per-batch form below
-                    const size_t o = (size_t)c * n + u;
-                    const int64_t t_last = t + run - 1;
-                    atomicMax((unsigned long long *)(p.last_flipped + o), (unsigned long long)t_last);
-                    atomicAdd((unsigned long long *)(p.part_sum + o), (unsigned long long)((lab_o - lab_t) * t_last));
-                    atomicAdd((unsigned long long *)(p.num_flips + o), (unsigned long long)run);
-                }
-                if (p.diag & FC_DIAG_FLIPS_EXACT) {
-                    const size_t o = (size_t)c * n + u;
-                    atomicAdd((unsigned long long *)(p.flip_count + o), 1ull);
-                    atomicAdd((unsigned long long *)(p.occ_acc + o), (unsigned long long)(-(lab_t - lab_o) * t));
-                    atomicMax((unsigned long long *)(p.last_accept + o), (unsigned long long)t);
-                }
-                if (p.diag & FC_DIAG_EDGES) {
-                    int64_t *ea = p.edge_acc + (size_t)c * p.n_edges;
-#pragma unroll
-                    for (int i = 0; i < RMAX; ++i)
-                        if (eid[i] >= 0) atomicAdd((unsigned long long *)(ea + eid[i]), (unsigned long long)(((up >> i) & 1u) ? -t : t));
+            if (p.diag & (FC_DIAG_HIST | FC_DIAG_FLIPS | FC_DIAG_FLIPS_EXACT | FC_DIAG_EDGES)) {
+                // the entries go to the chain's tally log (two coalesced stores; tally_reduce applies
+                // them after the launch): issued here, the atomics held up the next batch's first
+                // vector-memory wait (vmcnt counts them and completes in order), C2 full diagnostics
+                // 62.6 -> 54.8 ms per launch (profiles/r05e_tally_log_ab.txt).  A full log: atomics.
+                const int64_t lbase = (int64_t)misc[3];
+                if (p.tl && lbase + qn <= p.tl_cap) {
+                    if (in)
+                        ((uint4 *)p.tl)[(size_t)c * (size_t)p.tl_cap + (size_t)(lbase + lane)] =
+                            tally_pack(t - (int64_t)misc[4], run, qv, qc, (uint32_t)nbq);
+                    if (lane == 0) misc[3] = (uint64_t)(lbase + qn);
+                } else if (in) {
+                    tally_apply<RMAX>(p, c, t, run, qv, qc, (uint32_t)nbq, p.labels[0], p.labels[1]);
                 }
             }
             if (p.diag & FC_DIAG_SERIES) ev_len += qn;
@@ -283,6 +488,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     };
     int prio = 0;  // bits 0-1: the issue priority set; bits 2 and up: batches since it was last chosen
     if (lane == 0) {
+        misc[3] = 0;  // the tally log starts empty (tally_reduce emptied it)
+        misc[4] = (uint64_t)steps;
+        if (FULL && p.tl_t0) p.tl_t0[c] = steps;
         misc[0] = __builtin_amdgcn_s_memrealtime();
         // the previous launch's slowest-chain pace, scaled to this launch (0: none yet)
         const float eta0 = p.eta ? (float)p.eta[p.eta_parity ^ 1] * (float)p.n_steps * (1.0f / 1024.0f) : 0.0f;
@@ -1084,17 +1292,17 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         if constexpr (FULL) {
             // the run of the batch's start state goes on: a queued state takes it into its run
             // (below), else it is tallied here
-            if (lane == 0 && r0 && (!defer || qn == 0)) {
-                if (p.diag & FC_DIAG_HIST) {
-                    atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut0], (unsigned long long)r0);
-                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb0], (unsigned long long)r0);
-                }
-                if ((p.diag & FC_DIAG_FLIPS) && last_flip0 >= 0) {
-                    const int64_t lab0 = p.labels[0], lab1 = p.labels[1];
-                    const size_t o = (size_t)c * n + last_flip0;
-                    atomicMax((unsigned long long *)(p.last_flipped + o), (unsigned long long)(steps0 + r0));
-                    atomicAdd((unsigned long long *)(p.part_sum + o), (unsigned long long)((a_last0 ? lab0 - lab1 : lab1 - lab0) * r0));
-                    atomicAdd((unsigned long long *)(p.num_flips + o), (unsigned long long)r0);
+            if (lane == 0 && r0 && (!defer || qn == 0) && (p.diag & (FC_DIAG_HIST | FC_DIAG_FLIPS))) {
+                // (kind 1 of tally_apply: to the tally log like the queue entries, else applied here)
+                const uint32_t qv0 = (last_flip0 >= 0 ? (uint32_t)last_flip0 : 0xffffu) | ((uint32_t)(a_last0 & 1) << 16);
+                const int64_t lbase = (int64_t)misc[3];
+                if (p.tl && lbase < p.tl_cap) {
+                    ((uint4 *)p.tl)[(size_t)c * (size_t)p.tl_cap + (size_t)lbase] =
+                        tally_pack(steps0 - (int64_t)misc[4], r0, qv0, (uint32_t)cut0, (uint32_t)nb0 | 0x80000000u);
+                    misc[3] = (uint64_t)(lbase + 1);
+                } else {
+                    tally_apply<RMAX>(p, c, steps0, r0, qv0, (uint32_t)cut0, (uint32_t)nb0 | 0x80000000u, p.labels[0],
+                                      p.labels[1]);
                 }
             }
         }
@@ -1272,6 +1480,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         acc_cut2 += __shfl_xor((long long)acc_cut2, off);
         acc_nb2 += __shfl_xor((long long)acc_nb2, off);
     }
+    if (FULL && p.tl_len && lane == 0) p.tl_len[c] = (int64_t)misc[3];
     if (lane == 0) {
         scp->draw = draw;
         scp->steps = steps;

@@ -158,6 +158,14 @@ struct KParams {
     // k = 2 band stream (FC_STREAM_BAND): per chain the band S = b_nodes + neighbours as a
     // bitmap of `words` u64; a draw selects the i-th member (fc_flip2.hip)
     int32_t multi_flip;         // k > 2 district-rule instance: several independent flips per commit pass
+    // k = 2 full diagnostics: the per-flip tallies of the flushed wait / tally queue, logged per
+    // chain (two coalesced stores per entry) and applied by tally_reduce after the launch, so
+    // the chain's serial stream carries no global atomics (fc_flip2.hip tally_flush).  A full
+    // log falls back to the atomics; tl_len is 0 at every launch start (tally_reduce resets it)
+    uint32_t *tl;               // [n_chains * tl_cap][4], 16 B per entry (fc_flip2.hip tally_pack)
+    int64_t *tl_t0;             // [n_chains] yield index at the launch's start (entries hold t - t0)
+    int64_t *tl_len;            // [n_chains] entries logged this launch
+    int64_t tl_cap;             // entries per chain
     int32_t band;
     int32_t band_step0;         // largest power of two below `words` (rank search over the words)
     uint64_t *sbits;            // [n_chains * words]
@@ -203,6 +211,9 @@ int launch_recom(const RecomParams &p, int ring_max, void *stream, char *name, s
 // `name` (may be null) receives the launched instance, spelled as rocprofv3 reports it.
 int launch_flip_k2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap);  // k > 2
 int launch_flip2(const KParams &p, int ring_max, void *stream, char *name, size_t name_cap);    // k = 2
+// k = 2 full diagnostics: apply every chain's tally log (KParams tl_*) to the per-chain
+// histograms / per-node / per-edge arrays and reset the logs (fc_flip2.hip)
+int launch_tally_reduce(const KParams &p, int ring_max, void *stream);
 // chain dealing (fc_deal.hip): order[] = chains by descending key (ctime, the last launch's
 // draws, if `timed`, else the boundary length's complement n - |B|: a short boundary needs
 // many draws per proposal), and the deal counters zeroed, for the next flip launch
@@ -224,14 +235,17 @@ int launch_series_lagsums(const uint16_t *x, const int64_t *len, int32_t c0, int
 int launch_frame_series(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
                         const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
                         const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
-                        const uint64_t *tog_mask, int64_t cap, double *slope, double *angle, int32_t *cnt,
-                        void *stream);
+                        const uint64_t *tog_mask, int32_t n_rows, int32_t n_nodes, int64_t cap, double *slope,
+                        double *angle, int32_t *cnt, void *stream);
 // Change points of the same series (fc_run_frame_series_changes): cp_off == nullptr counts them
-// per chain into cp_cnt[cl]; otherwise writes (t, slope, angle) at cp_off[cl].
+// per chain into cp_cnt[cl]; otherwise writes (t, slope, angle) at cp_off[cl].  n_rows: rows of
+// tog_mask, n_nodes: entries of tog_idx (the tables are staged in LDS when they fit).
 int launch_frame_changes(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
                          const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
                          const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
-                         const uint64_t *tog_mask, const int64_t *t0, int64_t *cp_cnt, const int64_t *cp_off,
-                         int64_t *t_out, double *slope, double *angle, void *stream);
+                         const uint64_t *tog_mask, int32_t n_rows, int32_t n_nodes, const int64_t *t0,
+                         int64_t *cp_cnt, const int64_t *cp_off, int64_t *t_out, double *slope, double *angle,
+                         int64_t *wcnt, void *stream);
+constexpr int kFrameWaves = 4;  // waves per chain of the frame-series kernels (wcnt: [nc][kFrameWaves])
 
 }  // namespace fc

@@ -109,6 +109,24 @@ __device__ inline uint64_t shfl_up64(uint64_t x, int off) {
     return (uint64_t)__shfl_up((long long)x, off);
 }
 
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_x(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, false);
+}
+
+// inclusive prefix XOR over the 64 lanes (whole wave active): row_shr steps inside each 16-lane
+// row, then the row totals by the two row broadcasts (as fc_device.h wave_scan_incl)
+__device__ __forceinline__ uint64_t wave_xscan64(uint64_t v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo ^= dpp_x<0x111, 0xf>(lo); hi ^= dpp_x<0x111, 0xf>(hi);
+    lo ^= dpp_x<0x112, 0xf>(lo); hi ^= dpp_x<0x112, 0xf>(hi);
+    lo ^= dpp_x<0x114, 0xf>(lo); hi ^= dpp_x<0x114, 0xf>(hi);
+    lo ^= dpp_x<0x118, 0xf>(lo); hi ^= dpp_x<0x118, 0xf>(hi);
+    lo ^= dpp_x<0x142, 0xa>(lo); hi ^= dpp_x<0x142, 0xa>(hi);
+    lo ^= dpp_x<0x143, 0xc>(lo); hi ^= dpp_x<0x143, 0xc>(hi);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // slope and angle from the first two frame cut edges (canonical order); NaN with < 2
 __device__ inline void frame_eval(const uint64_t m[kFrameWords], const double *__restrict__ mid, double cx,
                                   double cy, double &slope, double &angle, int &cnt) {
@@ -145,30 +163,87 @@ __device__ inline void frame_eval(const uint64_t m[kFrameWords], const double *_
 
 // MODE 0: one (slope, angle, n_cut) entry per event, [cl * cap + i + 1] (entry 0: window start).
 // MODE 1: count the change points of (slope, angle) -- the window start and every event whose
-//         values differ bitwise from the previous entry's -- into cp_cnt[cl].
+//         values differ bitwise from the previous entry's -- into cp_cnt[cl] (and per wave into
+//         wcnt[cl * kFsWaves + w] for MODE 2).
 // MODE 2: write them at cp_off[cl]: (yield t at which the values start, slope, angle); the
 //         per-yield lists the reference plots (:476-484) are these values held to the next t.
-template <int MODE>
-__global__ __launch_bounds__(kThreads) void frame_series_kernel(
+// One workgroup of kFsWaves waves per chain: wave w takes a contiguous range of the chain's
+// 64-event chunks; a first pass XORs the toggle masks of each range (one table lookup per
+// event, no evaluation), so every wave knows the frame-cut mask at its range's start and the
+// ranges are evaluated in parallel.  LT: the toggle tables (node -> row as int16, row ->
+// frame-edge mask) and the midpoints are staged in LDS (sec11: 10.7 KB); the next chunk's events
+// are loaded before the current one is evaluated.
+constexpr int kFsWaves = kFrameWaves;
+
+template <int MODE, bool LT>
+__global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
     const int8_t *__restrict__ a0, int32_t npad, const fc_event *__restrict__ events, int64_t ev_cap,
     const int64_t *__restrict__ ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *__restrict__ fu,
     const int32_t *__restrict__ fv, const double *__restrict__ mid, double cx, double cy,
-    const int32_t *__restrict__ tog_idx, const uint64_t *__restrict__ tog_mask, int64_t cap,
-    double *__restrict__ slope_out, double *__restrict__ angle_out, int32_t *__restrict__ cnt_out,
+    const int32_t *__restrict__ tog_idx, const uint64_t *__restrict__ tog_mask, int32_t n_rows, int32_t n_nodes,
+    int64_t cap, double *__restrict__ slope_out, double *__restrict__ angle_out, int32_t *__restrict__ cnt_out,
     const int64_t *__restrict__ t0, int64_t *__restrict__ cp_cnt, const int64_t *__restrict__ cp_off,
-    int64_t *__restrict__ t_out) {
+    int64_t *__restrict__ t_out, int64_t *__restrict__ wcnt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint64_t sx[kFsWaves][kFrameWords];  // each range's XOR of toggle masks
+    __shared__ int64_t sn[kFsWaves];                 // MODE 1: each range's change points
     const int lane = threadIdx.x & 63;
-    const int32_t cl = (int32_t)(blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
-    if (cl >= nc) return;  // whole wave
+    const int w = (int)(threadIdx.x >> 6);
+    const double *md = mid;
+    const uint64_t *tm = tog_mask;
+    const int16_t *ti16 = nullptr;
+    if constexpr (LT) {
+        double *smid = (double *)smem;                                     // [2 n_frame]
+        uint64_t *stog = (uint64_t *)(smid + 2 * n_frame);                 // [n_rows][4]
+        int16_t *sidx = (int16_t *)(stog + (size_t)n_rows * kFrameWords);  // [n_nodes]
+        for (int i = threadIdx.x; i < 2 * n_frame; i += blockDim.x) smid[i] = mid[i];
+        for (int i = threadIdx.x; i < n_rows * kFrameWords; i += blockDim.x) stog[i] = tog_mask[i];
+        for (int i = threadIdx.x; i < n_nodes; i += blockDim.x) sidx[i] = (int16_t)tog_idx[i];
+        __syncthreads();
+        md = smid;
+        tm = stog;
+        ti16 = sidx;
+    }
+    const int32_t cl = (int32_t)blockIdx.x;
     const int32_t c = c0 + cl;
     const int8_t *a = a0 + (size_t)c * npad;
+    const fc_event *ev = events + (size_t)c * ev_cap;
+    const int64_t ne = ev_len[c];
+    auto row_of = [&](int v) -> int32_t { return LT ? (int32_t)ti16[v] : tog_idx[v]; };
+    // this wave's chunk range [k0, k1)
+    const int64_t nk = (ne + 63) >> 6;
+    const int64_t k0 = nk * w / kFsWaves, k1 = nk * (w + 1) / kFsWaves;
+    // pass 1: the XOR of the range's toggle masks
+    {
+        uint64_t x[kFrameWords] = {0, 0, 0, 0};
+        for (int64_t k = k0; k < k1; ++k) {
+            const int64_t i = 64 * k + lane;
+            if (i < ne) {
+                const int32_t r = row_of((int)ev[i].v);
+                if (r >= 0) {
+#pragma unroll
+                    for (int q = 0; q < kFrameWords; ++q) x[q] ^= tm[(size_t)r * kFrameWords + q];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kFrameWords; ++q) {
+            const uint64_t t = wave_xscan64(x[q]);
+            if (lane == 63) sx[w][q] = t;
+        }
+    }
+    // the window start's frame-cut mask, then this range's start
     uint64_t m[kFrameWords];
 #pragma unroll
-    for (int w = 0; w < kFrameWords; ++w) {
-        const int j = 64 * w + lane;
+    for (int q = 0; q < kFrameWords; ++q) {
+        const int j = 64 * q + lane;
         const bool cut = j < n_frame && a[fu[j]] != a[fv[j]];
-        m[w] = __ballot(cut);
+        m[q] = __ballot(cut);
     }
+    __syncthreads();
+    for (int w2 = 0; w2 < w; ++w2)
+#pragma unroll
+        for (int q = 0; q < kFrameWords; ++q) m[q] ^= sx[w2][q];
     double *so = slope_out, *ao = angle_out;
     int32_t *co = cnt_out;
     int64_t *to = t_out;
@@ -177,56 +252,66 @@ __global__ __launch_bounds__(kThreads) void frame_series_kernel(
         ao += (size_t)cl * cap;
         co += (size_t)cl * cap;
     } else if constexpr (MODE == 2) {
-        so += cp_off[cl];
-        ao += cp_off[cl];
-        to += cp_off[cl];
+        int64_t o = cp_off[cl];
+        for (int w2 = 0; w2 < w; ++w2) o += wcnt[(size_t)cl * kFsWaves + w2];
+        so += o;
+        ao += o;
+        to += o;
     }
-    // the previous entry's values (bit patterns: NaN == NaN), wave-uniform
+    // the values before the range's first event (bit patterns: NaN == NaN), wave-uniform; the
+    // window-start entry is wave 0's
     uint64_t prev_s, prev_a;
-    int64_t pos = 1;  // change points written (the window start is the first)
+    int64_t pos = 0;  // change points this wave writes
     {
         double sl, an;
         int cnt;
-        frame_eval(m, mid, cx, cy, sl, an, cnt);
+        frame_eval(m, md, cx, cy, sl, an, cnt);
         prev_s = (uint64_t)__double_as_longlong(sl);
         prev_a = (uint64_t)__double_as_longlong(an);
-        if (lane == 0) {
-            if constexpr (MODE == 0) {
-                so[0] = sl;
-                ao[0] = an;
-                co[0] = cnt;
-            } else if constexpr (MODE == 2) {
-                so[0] = sl;
-                ao[0] = an;
-                to[0] = t0[c];
+        if (w == 0) {
+            pos = 1;
+            if (lane == 0) {
+                if constexpr (MODE == 0) {
+                    so[0] = sl;
+                    ao[0] = an;
+                    co[0] = cnt;
+                } else if constexpr (MODE == 2) {
+                    so[0] = sl;
+                    ao[0] = an;
+                    to[0] = t0[c];
+                }
             }
         }
     }
-    const fc_event *ev = events + (size_t)c * ev_cap;
-    const int64_t ne = ev_len[c];
-    for (int64_t b = 0; b < ne; b += 64) {
+    // this lane's event of the next chunk, loaded one chunk ahead
+    int nv = 0;
+    int64_t nt = 0;
+    if (k0 < k1 && 64 * k0 + lane < ne) {
+        nv = (int)ev[64 * k0 + lane].v;
+        if (MODE == 2) nt = ev[64 * k0 + lane].t;
+    }
+    for (int64_t k = k0; k < k1; ++k) {
+        const int64_t b = 64 * k;
         const int64_t i = b + lane;
+        const int vcur = nv;
+        const int64_t tcur = nt;
+        if (k + 1 < k1 && b + 64 + lane < ne) {
+            nv = (int)ev[b + 64 + lane].v;
+            if (MODE == 2) nt = ev[b + 64 + lane].t;
+        }
         uint64_t t[kFrameWords] = {0, 0, 0, 0};
         if (i < ne) {
-            const int32_t s = tog_idx[ev[i].v];
-            if (s >= 0) {
+            const int32_t r = row_of(vcur);
+            if (r >= 0) {
 #pragma unroll
-                for (int w = 0; w < kFrameWords; ++w) t[w] = tog_mask[(size_t)s * kFrameWords + w];
+                for (int q = 0; q < kFrameWords; ++q) t[q] = tm[(size_t)r * kFrameWords + q];
             }
         }
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-#pragma unroll
-            for (int w = 0; w < kFrameWords; ++w) {
-                const uint64_t y = shfl_up64(t[w], off);
-                if (lane >= off) t[w] ^= y;
-            }
-        }
-#pragma unroll
-        for (int w = 0; w < kFrameWords; ++w) t[w] ^= m[w];
+        for (int q = 0; q < kFrameWords; ++q) t[q] = wave_xscan64(t[q]) ^ m[q];
         double sl = 0.0, an = 0.0;
         int cnt = 0;
-        if (i < ne) frame_eval(t, mid, cx, cy, sl, an, cnt);
+        if (i < ne) frame_eval(t, md, cx, cy, sl, an, cnt);
         if constexpr (MODE == 0) {
             if (i < ne) {
                 so[i + 1] = sl;
@@ -241,26 +326,42 @@ __global__ __launch_bounds__(kThreads) void frame_series_kernel(
                 pa = prev_a;
             }
             const bool chg = i < ne && (bs != ps || ba != pa);
-            const uint64_t cm = __ballot(chg);
+            const uint64_t cmk = __ballot(chg);
             if constexpr (MODE == 2) {
                 if (chg) {
-                    const int64_t o = pos + __popcll(cm & ((1ull << lane) - 1ull));
+                    const int64_t o = pos + __popcll(cmk & ((1ull << lane) - 1ull));
                     so[o] = sl;
                     ao[o] = an;
-                    to[o] = ev[i].t;
+                    to[o] = tcur;
                 }
             }
-            pos += __popcll(cm);
+            pos += __popcll(cmk);
             const int last = (int)((ne - b < 64 ? ne - b : 64) - 1);  // the chunk's last event
             prev_s = (uint64_t)__shfl((long long)bs, last);
             prev_a = (uint64_t)__shfl((long long)ba, last);
         }
 #pragma unroll
-        for (int w = 0; w < kFrameWords; ++w) m[w] = (uint64_t)__shfl((long long)t[w], 63);
+        for (int q = 0; q < kFrameWords; ++q) m[q] = (uint64_t)__shfl((long long)t[q], 63);
     }
     if constexpr (MODE == 1) {
-        if (lane == 0) cp_cnt[cl] = pos;
+        if (lane == 0) {
+            sn[w] = pos;
+            wcnt[(size_t)cl * kFsWaves + w] = pos;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t tot = 0;
+            for (int w2 = 0; w2 < kFsWaves; ++w2) tot += sn[w2];
+            cp_cnt[cl] = tot;
+        }
     }
+}
+
+// LDS bytes of the staged tables, or 0 when they do not fit (then the kernel reads them from
+// global memory)
+inline size_t frame_lds_bytes(int32_t n_frame, int32_t n_rows, int32_t n_nodes) {
+    const size_t b = 16 * (size_t)n_frame + 8 * kFrameWords * (size_t)n_rows + 2 * (size_t)n_nodes;
+    return (b <= 48 * 1024 && n_nodes < 32768) ? (b + 15) & ~(size_t)15 : 0;
 }
 
 }  // namespace
@@ -292,35 +393,52 @@ namespace fc {
 int launch_frame_series(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
                         const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
                         const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
-                        const uint64_t *tog_mask, int64_t cap, double *slope, double *angle, int32_t *cnt,
-                        void *stream) {
+                        const uint64_t *tog_mask, int32_t n_rows, int32_t n_nodes, int64_t cap, double *slope,
+                        double *angle, int32_t *cnt, void *stream) {
     if (nc <= 0) return (int)hipSuccess;
     if (n_frame > 64 * kFrameWords) return (int)hipErrorInvalidValue;
-    const int wpb = kThreads / 64;
-    const dim3 grid((unsigned)((nc + wpb - 1) / wpb));
-    hipLaunchKernelGGL(frame_series_kernel<0>, grid, dim3(kThreads), 0, (hipStream_t)stream, a0, npad, events,
-                       ev_cap, ev_len, c0, nc, n_frame, fu, fv, mid, cx, cy, tog_idx, tog_mask, cap, slope, angle, cnt,
-                       (const int64_t *)nullptr, (int64_t *)nullptr, (const int64_t *)nullptr, (int64_t *)nullptr);
+    const dim3 grid((unsigned)nc), block(64 * kFsWaves);
+    const size_t lds = frame_lds_bytes(n_frame, n_rows, n_nodes);
+#define FC_FS_ARGS a0, npad, events, ev_cap, ev_len, c0, nc, n_frame, fu, fv, mid, cx, cy, tog_idx, tog_mask, n_rows, n_nodes
+    if (lds)
+        hipLaunchKernelGGL((frame_series_kernel<0, true>), grid, block, lds, (hipStream_t)stream, FC_FS_ARGS,
+                           cap, slope, angle, cnt, (const int64_t *)nullptr, (int64_t *)nullptr,
+                           (const int64_t *)nullptr, (int64_t *)nullptr, (int64_t *)nullptr);
+    else
+        hipLaunchKernelGGL((frame_series_kernel<0, false>), grid, block, 0, (hipStream_t)stream, FC_FS_ARGS,
+                           cap, slope, angle, cnt, (const int64_t *)nullptr, (int64_t *)nullptr,
+                           (const int64_t *)nullptr, (int64_t *)nullptr, (int64_t *)nullptr);
     return (int)hipGetLastError();
 }
 
 int launch_frame_changes(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
                          const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
                          const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
-                         const uint64_t *tog_mask, const int64_t *t0, int64_t *cp_cnt, const int64_t *cp_off,
-                         int64_t *t_out, double *slope, double *angle, void *stream) {
+                         const uint64_t *tog_mask, int32_t n_rows, int32_t n_nodes, const int64_t *t0,
+                         int64_t *cp_cnt, const int64_t *cp_off, int64_t *t_out, double *slope, double *angle,
+                         int64_t *wcnt, void *stream) {
     if (nc <= 0) return (int)hipSuccess;
     if (n_frame > 64 * kFrameWords) return (int)hipErrorInvalidValue;
-    const int wpb = kThreads / 64;
-    const dim3 grid((unsigned)((nc + wpb - 1) / wpb));
-    if (!cp_off)
-        hipLaunchKernelGGL(frame_series_kernel<1>, grid, dim3(kThreads), 0, (hipStream_t)stream, a0, npad, events,
-                           ev_cap, ev_len, c0, nc, n_frame, fu, fv, mid, cx, cy, tog_idx, tog_mask, (int64_t)0,
-                           (double *)nullptr, (double *)nullptr, (int32_t *)nullptr, t0, cp_cnt, cp_off, t_out);
-    else
-        hipLaunchKernelGGL(frame_series_kernel<2>, grid, dim3(kThreads), 0, (hipStream_t)stream, a0, npad, events,
-                           ev_cap, ev_len, c0, nc, n_frame, fu, fv, mid, cx, cy, tog_idx, tog_mask, (int64_t)0, slope,
-                           angle, (int32_t *)nullptr, t0, cp_cnt, cp_off, t_out);
+    const dim3 grid((unsigned)nc), block(64 * kFsWaves);
+    const size_t lds = frame_lds_bytes(n_frame, n_rows, n_nodes);
+    if (!cp_off) {
+        if (lds)
+            hipLaunchKernelGGL((frame_series_kernel<1, true>), grid, block, lds, (hipStream_t)stream, FC_FS_ARGS,
+                               (int64_t)0, (double *)nullptr, (double *)nullptr, (int32_t *)nullptr, t0, cp_cnt, cp_off,
+                               t_out, wcnt);
+        else
+            hipLaunchKernelGGL((frame_series_kernel<1, false>), grid, block, 0, (hipStream_t)stream, FC_FS_ARGS,
+                               (int64_t)0, (double *)nullptr, (double *)nullptr, (int32_t *)nullptr, t0, cp_cnt, cp_off,
+                               t_out, wcnt);
+    } else {
+        if (lds)
+            hipLaunchKernelGGL((frame_series_kernel<2, true>), grid, block, lds, (hipStream_t)stream, FC_FS_ARGS,
+                               (int64_t)0, slope, angle, (int32_t *)nullptr, t0, cp_cnt, cp_off, t_out, wcnt);
+        else
+            hipLaunchKernelGGL((frame_series_kernel<2, false>), grid, block, 0, (hipStream_t)stream, FC_FS_ARGS,
+                               (int64_t)0, slope, angle, (int32_t *)nullptr, t0, cp_cnt, cp_off, t_out, wcnt);
+    }
+#undef FC_FS_ARGS
     return (int)hipGetLastError();
 }
 

@@ -203,15 +203,6 @@ def test_sharded_equals_unsharded(gpu, sec11):
         assert np.array_equal(part.state(), fa[off:off + cnt])
 
 
-# (k = 2 node stream: no round cut-off -- tune_hit_stop is refused there; the band stream's
-# shapes with it are in tests/test_band_gpu.py)
-@pytest.mark.parametrize("nsub,hit_stop,extra", [(1, 0, {}), (2, 0, {}), (4, 0, {}),
-                                               (4, 0, {"wait_queue": 1}), (4, 0, {"wait_queue": 3}),
-                                               (4, 0, {"par_min": 65}), (4, 0, {"par_min": 1}),
-                                               (4, 0, {"chains_per_block": 4}), (4, 0, {"deal": 1}),
-                                               (4, 0, {"prio_div": (-1, 0, 0)}),
-                                               (2, 0, {"prio_th": (-1.0, 0.0, 0.0)})])
-@pytest.mark.parametrize("lean", [True, False])
 def test_hit_stop_refused_on_k2_node_stream(gpu, sec11):
     """The k = 2 node stream's batch window is 64 * nsub draws closed by the 64th hit: a round
     cut-off would change nothing, so a nonzero tune_hit_stop is an argument error there (ADVICE
@@ -223,6 +214,15 @@ def test_hit_stop_refused_on_k2_node_stream(gpu, sec11):
     FlipRun(FlipGraph(sec11), a0, RunConfig(seed=1, pop_lo=lo, pop_hi=hi, stream="band", tune={"hit_stop": 24}))
 
 
+# (k = 2 node stream: no round cut-off -- tune_hit_stop is refused there; the band stream's
+# shapes with it are in tests/test_band_gpu.py)
+@pytest.mark.parametrize("nsub,hit_stop,extra", [(1, 0, {}), (2, 0, {}), (4, 0, {}),
+                                               (4, 0, {"wait_queue": 1}), (4, 0, {"wait_queue": 3}),
+                                               (4, 0, {"par_min": 65}), (4, 0, {"par_min": 1}),
+                                               (4, 0, {"chains_per_block": 4}), (4, 0, {"deal": 1}),
+                                               (4, 0, {"prio_div": (-1, 0, 0)}),
+                                               (2, 0, {"prio_th": (-1.0, 0.0, 0.0)})])
+@pytest.mark.parametrize("lean", [True, False])
 def test_sec11_batch_shapes(gpu, cref, sec11, nsub, hit_stop, extra, lean):
     """Every launch-tuning field of fc_params the k = 2 node stream takes (draw rounds per batch
     ``tune_nsub``, the deferred-wait queue length, the segment-parallel threshold,
