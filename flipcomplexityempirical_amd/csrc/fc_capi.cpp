@@ -79,6 +79,9 @@ struct fc_run {
     uint64_t fc_frame_hash = 0;
     int32_t fc_rows = 0;  // rows of d_fc_tog
     int64_t *d_fc_wcnt = nullptr;  // change points per chain and frame-series wave
+    int64_t *d_st_t = nullptr;     // one-pass change points: per-wave staging ranges (t; slope, angle)
+    double *d_st_sa = nullptr;
+    size_t fc_stage_cap = 0;
     int32_t *d_fc_fuv = nullptr, *d_fc_tidx = nullptr;
     uint64_t *d_fc_tog = nullptr;
     double *d_fc_mid = nullptr;
@@ -129,7 +132,7 @@ void free_run(fc_run *r) {
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
                     r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_nfh, r->d_sbits, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh, r->d_tl, r->d_tl_len, r->d_tl_t0,
                     r->d_fs_out, r->d_fs_cnt, r->d_fc_fuv, r->d_fc_tidx, r->d_fc_tog, r->d_fc_mid, r->d_fc_len,
-                    r->d_fc_t0, r->d_fc_cnt, r->d_fc_off, r->d_fc_t, r->d_fc_sa, r->d_fc_wcnt};
+                    r->d_fc_t0, r->d_fc_cnt, r->d_fc_off, r->d_fc_t, r->d_fc_sa, r->d_fc_wcnt, r->d_st_t, r->d_st_sa};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &pr : r->launch_events) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -1615,11 +1618,43 @@ int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_fra
     HIP_TRY(hipMemcpyAsync(r->d_fc_len + c0, ev_len.data(), (size_t)nc * 8, hipMemcpyHostToDevice, r->stream));
     HIP_TRY(hipMemcpyAsync(r->d_fc_t0 + c0, t0.data(), (size_t)nc * 8, hipMemcpyHostToDevice, r->stream));
     int32_t *const d_fuv = r->d_fc_fuv;
-    // pass 1: change points per chain -> offsets
-    int e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, r->d_fc_len, c0, nc, n_frame, d_fuv,
+    // one pass (count and write together) into per-wave staging ranges when they fit a tenth of
+    // the free device memory: sized by event_cap, kept by the run
+    const int64_t nk = (r->ev_cap + 63) / 64;
+    const int64_t sub = 64 * ((nk + fc::kFrameWaves - 1) / fc::kFrameWaves) + 1;
+    const int64_t stage_cap = sub * fc::kFrameWaves;
+    bool staged = false;
+    if (!query) {
+        const size_t want = (size_t)r->n_chains * (size_t)stage_cap;
+        if (want > r->fc_stage_cap) {
+            size_t free_b = 0, total_b = 0;
+            HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+            if (want * 24 <= free_b / 10) {
+                for (void *b : {(void *)r->d_st_t, (void *)r->d_st_sa})
+                    if (b) (void)hipFree(b);
+                r->d_st_t = nullptr;
+                r->d_st_sa = nullptr;
+                r->fc_stage_cap = 0;
+                if ((q = dalloc(&r->d_st_t, want))) return q;
+                if ((q = dalloc(&r->d_st_sa, 2 * want))) return q;
+                r->fc_stage_cap = want;
+            }
+        }
+        staged = want <= r->fc_stage_cap;
+    }
+    const size_t stn = r->fc_stage_cap;  // staging: slope at d_st_sa, angle at d_st_sa + stn
+    int e;
+    if (staged)
+        e = fc::launch_frame_stage(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, r->d_fc_len, c0, nc, n_frame, d_fuv,
+                                   d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->fc_rows, n,
+                                   r->d_fc_t0, r->d_fc_cnt, stage_cap, r->d_st_t, r->d_st_sa, r->d_st_sa + stn,
+                                   r->d_fc_wcnt, r->stream);
+    else  // pass 1: change points per chain -> offsets
+        e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, r->d_fc_len, c0, nc, n_frame, d_fuv,
                                      d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->fc_rows, n,
                                      r->d_fc_t0, r->d_fc_cnt, nullptr, nullptr, nullptr, nullptr, r->d_fc_wcnt, r->stream);
-    if (e) return fail(FC_ERR_HIP, std::string("frame changes (count): ") + hipGetErrorString((hipError_t)e));
+    if (e) return fail(FC_ERR_HIP, std::string(staged ? "frame changes (stage): " : "frame changes (count): ") +
+                                       hipGetErrorString((hipError_t)e));
     std::vector<int64_t> cnt(nc);
     HIP_TRY(hipMemcpyAsync(cnt.data(), r->d_fc_cnt, (size_t)nc * 8, hipMemcpyDeviceToHost, r->stream));
     HIP_TRY(hipStreamSynchronize(r->stream));
@@ -1643,9 +1678,13 @@ int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_fra
     // pass 2: (t, slope, angle) at the offsets, then one copy per array
     HIP_TRY(hipMemcpyAsync(r->d_fc_off, offsets, (size_t)nc * 8, hipMemcpyHostToDevice, r->stream));
     double *const d_sl = r->d_fc_sa, *const d_an = r->d_fc_sa + r->fc_cap;
-    e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, r->d_fc_len, c0, nc, n_frame, d_fuv,
-                                 d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->fc_rows, n,
-                                 r->d_fc_t0, r->d_fc_cnt, r->d_fc_off, r->d_fc_t, d_sl, d_an, r->d_fc_wcnt, r->stream);
+    if (staged)  // the staged ranges packed at the offsets
+        e = fc::launch_frame_compact(nc, stage_cap, r->d_st_t, r->d_st_sa, r->d_st_sa + stn, r->d_fc_wcnt, r->d_fc_off,
+                                     r->d_fc_t, d_sl, d_an, r->stream);
+    else
+        e = fc::launch_frame_changes(r->d_ser_a0, r->npad, r->d_events, r->ev_cap, r->d_fc_len, c0, nc, n_frame, d_fuv,
+                                     d_fuv + n_frame, r->d_fc_mid, cx, cy, r->d_fc_tidx, r->d_fc_tog, r->fc_rows, n,
+                                     r->d_fc_t0, r->d_fc_cnt, r->d_fc_off, r->d_fc_t, d_sl, d_an, r->d_fc_wcnt, r->stream);
     if (e) return fail(FC_ERR_HIP, std::string("frame changes (write): ") + hipGetErrorString((hipError_t)e));
     HIP_TRY(hipMemcpyAsync(t, r->d_fc_t, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));
     HIP_TRY(hipMemcpyAsync(slope, d_sl, (size_t)total * 8, hipMemcpyDeviceToHost, r->stream));

@@ -247,5 +247,18 @@ int launch_frame_changes(const int8_t *a0, int32_t npad, const fc_event *events,
                          int64_t *cp_cnt, const int64_t *cp_off, int64_t *t_out, double *slope, double *angle,
                          int64_t *wcnt, void *stream);
 constexpr int kFrameWaves = 4;  // waves per chain of the frame-series kernels (wcnt: [nc][kFrameWaves])
+// One-pass form of the above (count and write together): each chain's waves stage their change
+// points at st_* + cl * stage_cap + w * (stage_cap / kFrameWaves), counts in wcnt / cp_cnt; then
+// launch_frame_compact packs them at cp_off.  stage_cap / kFrameWaves must exceed the events of any
+// wave's range: 64 * ceil(ceil(ev_cap / 64) / kFrameWaves) + 1.
+int launch_frame_stage(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
+                       const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
+                       const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
+                       const uint64_t *tog_mask, int32_t n_rows, int32_t n_nodes, const int64_t *t0,
+                       int64_t *cp_cnt, int64_t stage_cap, int64_t *st_t, double *st_s, double *st_a,
+                       int64_t *wcnt, void *stream);
+int launch_frame_compact(int32_t nc, int64_t stage_cap, const int64_t *st_t, const double *st_s,
+                         const double *st_a, const int64_t *wcnt, const int64_t *cp_off, int64_t *t_out,
+                         double *slope, double *angle, void *stream);
 
 }  // namespace fc

@@ -167,6 +167,9 @@ __device__ inline void frame_eval(const uint64_t m[kFrameWords], const double *_
 //         wcnt[cl * kFsWaves + w] for MODE 2).
 // MODE 2: write them at cp_off[cl]: (yield t at which the values start, slope, angle); the
 //         per-yield lists the reference plots (:476-484) are these values held to the next t.
+// MODE 3: MODE 1 and 2 in one pass: each wave writes its change points to its own staging
+//         range (t_out / slope_out / angle_out + cl * cap + w * (cap / kFsWaves)) and its count
+//         to wcnt; frame_compact_kernel then packs them at the chain offsets.
 // One workgroup of kFsWaves waves per chain: wave w takes a contiguous range of the chain's
 // 64-event chunks; a first pass XORs the toggle masks of each range (one table lookup per
 // event, no evaluation), so every wave knows the frame-cut mask at its range's start and the
@@ -257,6 +260,11 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
         so += o;
         ao += o;
         to += o;
+    } else if constexpr (MODE == 3) {
+        const size_t o = (size_t)cl * (size_t)cap + (size_t)w * (size_t)(cap / kFsWaves);
+        so += o;
+        ao += o;
+        to += o;
     }
     // the values before the range's first event (bit patterns: NaN == NaN), wave-uniform; the
     // window-start entry is wave 0's
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
                     so[0] = sl;
                     ao[0] = an;
                     co[0] = cnt;
-                } else if constexpr (MODE == 2) {
+                } else if constexpr (MODE >= 2) {
                     so[0] = sl;
                     ao[0] = an;
                     to[0] = t0[c];
@@ -288,7 +296,7 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
     int64_t nt = 0;
     if (k0 < k1 && 64 * k0 + lane < ne) {
         nv = (int)ev[64 * k0 + lane].v;
-        if (MODE == 2) nt = ev[64 * k0 + lane].t;
+        if (MODE >= 2) nt = ev[64 * k0 + lane].t;
     }
     for (int64_t k = k0; k < k1; ++k) {
         const int64_t b = 64 * k;
@@ -297,7 +305,7 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
         const int64_t tcur = nt;
         if (k + 1 < k1 && b + 64 + lane < ne) {
             nv = (int)ev[b + 64 + lane].v;
-            if (MODE == 2) nt = ev[b + 64 + lane].t;
+            if (MODE >= 2) nt = ev[b + 64 + lane].t;
         }
         uint64_t t[kFrameWords] = {0, 0, 0, 0};
         if (i < ne) {
@@ -327,7 +335,7 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
             }
             const bool chg = i < ne && (bs != ps || ba != pa);
             const uint64_t cmk = __ballot(chg);
-            if constexpr (MODE == 2) {
+            if constexpr (MODE >= 2) {
                 if (chg) {
                     const int64_t o = pos + __popcll(cmk & ((1ull << lane) - 1ull));
                     so[o] = sl;
@@ -343,7 +351,7 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
 #pragma unroll
         for (int q = 0; q < kFrameWords; ++q) m[q] = (uint64_t)__shfl((long long)t[q], 63);
     }
-    if constexpr (MODE == 1) {
+    if constexpr (MODE == 1 || MODE == 3) {
         if (lane == 0) {
             sn[w] = pos;
             wcnt[(size_t)cl * kFsWaves + w] = pos;
@@ -354,6 +362,28 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
             for (int w2 = 0; w2 < kFsWaves; ++w2) tot += sn[w2];
             cp_cnt[cl] = tot;
         }
+    }
+}
+
+// MODE 3's staging ranges packed at the chains' offsets: chain cl's wave w range (wcnt[cl][w]
+// entries at cl * cap + w * (cap / kFsWaves)) goes to cp_off[cl] + the counts of waves < w.
+__global__ __launch_bounds__(kThreads) void frame_compact_kernel(const int64_t *__restrict__ st_t,
+                                                                 const double *__restrict__ st_s,
+                                                                 const double *__restrict__ st_a, int64_t cap,
+                                                                 const int64_t *__restrict__ wcnt,
+                                                                 const int64_t *__restrict__ cp_off, int64_t *t_out,
+                                                                 double *slope, double *angle) {
+    const int32_t cl = (int32_t)blockIdx.x;
+    int64_t dst = cp_off[cl];
+    for (int w = 0; w < kFsWaves; ++w) {
+        const int64_t n = wcnt[(size_t)cl * kFsWaves + w];
+        const size_t src = (size_t)cl * (size_t)cap + (size_t)w * (size_t)(cap / kFsWaves);
+        for (int64_t i = threadIdx.x; i < n; i += kThreads) {
+            t_out[dst + i] = st_t[src + i];
+            slope[dst + i] = st_s[src + i];
+            angle[dst + i] = st_a[src + i];
+        }
+        dst += n;
     }
 }
 
@@ -438,8 +468,38 @@ int launch_frame_changes(const int8_t *a0, int32_t npad, const fc_event *events,
             hipLaunchKernelGGL((frame_series_kernel<2, false>), grid, block, 0, (hipStream_t)stream, FC_FS_ARGS,
                                (int64_t)0, slope, angle, (int32_t *)nullptr, t0, cp_cnt, cp_off, t_out, wcnt);
     }
-#undef FC_FS_ARGS
     return (int)hipGetLastError();
 }
+
+int launch_frame_stage(const int8_t *a0, int32_t npad, const fc_event *events, int64_t ev_cap,
+                       const int64_t *ev_len, int32_t c0, int32_t nc, int32_t n_frame, const int32_t *fu,
+                       const int32_t *fv, const double *mid, double cx, double cy, const int32_t *tog_idx,
+                       const uint64_t *tog_mask, int32_t n_rows, int32_t n_nodes, const int64_t *t0,
+                       int64_t *cp_cnt, int64_t stage_cap, int64_t *st_t, double *st_s, double *st_a,
+                       int64_t *wcnt, void *stream) {
+    if (nc <= 0) return (int)hipSuccess;
+    if (n_frame > 64 * kFrameWords) return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)nc), block(64 * kFsWaves);
+    const size_t lds = frame_lds_bytes(n_frame, n_rows, n_nodes);
+    if (lds)
+        hipLaunchKernelGGL((frame_series_kernel<3, true>), grid, block, lds, (hipStream_t)stream, FC_FS_ARGS,
+                           stage_cap, st_s, st_a, (int32_t *)nullptr, t0, cp_cnt, (const int64_t *)nullptr, st_t,
+                           wcnt);
+    else
+        hipLaunchKernelGGL((frame_series_kernel<3, false>), grid, block, 0, (hipStream_t)stream, FC_FS_ARGS,
+                           stage_cap, st_s, st_a, (int32_t *)nullptr, t0, cp_cnt, (const int64_t *)nullptr, st_t,
+                           wcnt);
+    return (int)hipGetLastError();
+}
+
+int launch_frame_compact(int32_t nc, int64_t stage_cap, const int64_t *st_t, const double *st_s,
+                         const double *st_a, const int64_t *wcnt, const int64_t *cp_off, int64_t *t_out,
+                         double *slope, double *angle, void *stream) {
+    if (nc <= 0) return (int)hipSuccess;
+    hipLaunchKernelGGL(frame_compact_kernel, dim3((unsigned)nc), dim3(kThreads), 0, (hipStream_t)stream, st_t, st_s,
+                       st_a, stage_cap, wcnt, cp_off, t_out, slope, angle);
+    return (int)hipGetLastError();
+}
+#undef FC_FS_ARGS
 
 }  // namespace fc
