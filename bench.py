@@ -693,6 +693,7 @@ def main():
         f0 = rf.stats()
         rf.timings()
         t_series, n_events, n_nan, n_changes, n_cp_fallback = 0.0, 0, 0, 0, 0
+        t_checks = 0.0  # the bench line's own counts / NaN scan of the series (not the reference's work)
         t_pe, n_pe = 0.0, 0   # the per-event form, measured on the last launch only (outside the rates)
         t_acf, acf_out = 0.0, None
         fs_buf = None
@@ -717,13 +718,17 @@ def main():
                 # (:476-484): change points (t, slope, angle) of every chain, on the device, one
                 # copy per array into pinned host buffers reused over the launches
                 ch = rf.frame_series_changes(frame, out=cp_buf)
+                t_series += time.perf_counter() - ts
+                # the line's own checks (counts for the JSON, a scan of the angles): outside both
+                # rates, timed apart
+                tc = time.perf_counter()
                 n_changes += int(ch["offsets"][-1])
                 # more change points than the pinned buffers hold: a second native call into
                 # fresh unpinned arrays (counted)
                 n_cp_fallback += int(ch["offsets"][-1] > cp_buf["t"].size)
                 n_events += int(rf.stats()["events"].sum())
                 n_nan += int(np.isnan(ch["angle"]).sum())
-                t_series += time.perf_counter() - ts
+                t_checks += time.perf_counter() - tc
                 if it == n_full - 1:
                     # beside it, once: the per-event form (every event's slope / angle / frame-cut
                     # count) copied to the host in chunks of 256 chains
@@ -738,7 +743,7 @@ def main():
                     t_pe += time.perf_counter() - tp
                 rf.series_reset()
         barrier_sync_f()
-        dtf = D.allreduce_max(time.perf_counter() - t0f - t_pe, dist, dev)
+        dtf = D.allreduce_max(time.perf_counter() - t0f - t_pe - t_checks, dist, dev)
         if cp_buf is not None:
             for b_ in cp_buf.values():
                 unpin_host(b_)
@@ -774,6 +779,10 @@ def main():
                                      "pinned_buffer_entries": int(cp_buf["t"].size) if cp_buf else None,
                                      "events_per_s": n_events / t_series if t_series else None,
                                      "nan_angles_at_change_points": n_nan,
+                                     "bench_checks_ms_per_launch": t_checks / max(n_full, 1) * 1e3,
+                                     "bench_checks_note": "the line's own counts (events from the chain "
+                                                          "records) and the NaN scan of the angles, timed apart "
+                                                          "and outside both rates",
                                      "note": "fc_run_frame_series_changes over all chains after every launch: the "
                                              "(t, slope, angle) change points of the reference's per-yield slope / "
                                              "angle lists (:371-394), bitwise those lists when held over their "

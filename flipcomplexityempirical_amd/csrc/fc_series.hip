@@ -127,10 +127,11 @@ __device__ __forceinline__ uint64_t wave_xscan64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// slope and angle from the first two frame cut edges (canonical order); NaN with < 2
-__device__ inline void frame_eval(const uint64_t m[kFrameWords], const double *__restrict__ mid, double cx,
-                                  double cy, double &slope, double &angle, int &cnt) {
-#pragma clang fp contract(off)
+// The values depend on the frame-cut mask only through its first two cut edges (canonical
+// order): the key j0 | j1 << 16, or kNoPair with fewer than two (NaN values)
+constexpr uint32_t kNoPair = 0xffffffffu;
+
+__device__ inline uint32_t frame_key(const uint64_t m[kFrameWords], int &cnt) {
     int j0 = -1, j1 = -1;
     cnt = 0;
 #pragma unroll
@@ -145,11 +146,19 @@ __device__ inline void frame_eval(const uint64_t m[kFrameWords], const double *_
             if (x) j1 = 64 * w + __builtin_ctzll(x);
         }
     }
-    if (cnt < 2) {  // the reference raises IndexError on temp[1] here
+    return cnt < 2 ? kNoPair : (uint32_t)j0 | ((uint32_t)j1 << 16);
+}
+
+// slope and angle of a key
+__device__ inline void key_eval(uint32_t key, const double *__restrict__ mid, double cx, double cy, double &slope,
+                                double &angle) {
+#pragma clang fp contract(off)
+    if (key == kNoPair) {  // the reference raises IndexError on temp[1] here
         slope = __builtin_nan("");
         angle = __builtin_nan("");
         return;
     }
+    const int j0 = (int)(key & 0xffffu), j1 = (int)(key >> 16);
     const double ax = mid[2 * j0], ay = mid[2 * j0 + 1], bx = mid[2 * j1], by = mid[2 * j1 + 1];
     // slope = (endb[1]-enda[1])/(endb[0]-enda[0]) else np.Inf  (:378-382)
     slope = (bx != ax) ? (by - ay) / (bx - ax) : __builtin_inf();
@@ -159,6 +168,11 @@ __device__ inline void frame_eval(const uint64_t m[kFrameWords], const double *_
     double d = (pax / na) * (pbx / nb) + (pay / na) * (pby / nb);
     d = d < -1.0 ? -1.0 : (d > 1.0 ? 1.0 : d);
     angle = acos(d);
+}
+
+__device__ inline void frame_eval(const uint64_t m[kFrameWords], const double *__restrict__ mid, double cx,
+                                  double cy, double &slope, double &angle, int &cnt) {
+    key_eval(frame_key(m, cnt), mid, cx, cy, slope, angle);
 }
 
 // MODE 0: one (slope, angle, n_cut) entry per event, [cl * cap + i + 1] (entry 0: window start).
@@ -269,11 +283,13 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
     // the values before the range's first event (bit patterns: NaN == NaN), wave-uniform; the
     // window-start entry is wave 0's
     uint64_t prev_s, prev_a;
+    uint32_t prev_key;  // MODE >= 1: the key of the event before this lane's (the range start's)
     int64_t pos = 0;  // change points this wave writes
     {
         double sl, an;
         int cnt;
-        frame_eval(m, md, cx, cy, sl, an, cnt);
+        prev_key = frame_key(m, cnt);
+        key_eval(prev_key, md, cx, cy, sl, an);
         prev_s = (uint64_t)__double_as_longlong(sl);
         prev_a = (uint64_t)__double_as_longlong(an);
         if (w == 0) {
@@ -291,6 +307,54 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
             }
         }
     }
+    // MODE >= 1: the queued candidate events (key, yield) of this wave, and their evaluation:
+    // values against the previous entry's (the last evaluated one before them), change points
+    // written / counted in order
+    __shared__ uint32_t qk[kFsWaves][128];
+    __shared__ int64_t qt[kFsWaves][128];
+    int qn = 0;
+    auto flush = [&](int nq) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the queue entries other lanes wrote
+        const bool on = lane < nq;
+        const uint32_t k = on ? qk[w][lane] : kNoPair;
+        int64_t tq = 0;
+        if constexpr (MODE >= 2) tq = on ? qt[w][lane] : 0;
+        double sl, an;
+        key_eval(k, md, cx, cy, sl, an);
+        const uint64_t bs = (uint64_t)__double_as_longlong(sl), ba = (uint64_t)__double_as_longlong(an);
+        uint64_t ps = shfl_up64(bs, 1), pa = shfl_up64(ba, 1);
+        if (lane == 0) {
+            ps = prev_s;
+            pa = prev_a;
+        }
+        const bool chg = on && (bs != ps || ba != pa);
+        const uint64_t cmk = __ballot(chg);
+        if constexpr (MODE >= 2) {
+            if (chg) {
+                const int64_t o = pos + __popcll(cmk & ((1ull << lane) - 1ull));
+                so[o] = sl;
+                ao[o] = an;
+                to[o] = tq;
+            }
+        }
+        pos += __popcll(cmk);
+        prev_s = (uint64_t)__shfl((long long)bs, nq - 1);
+        prev_a = (uint64_t)__shfl((long long)ba, nq - 1);
+        // the entries after the first nq move to the front (reads of [nq, qn), writes of [0, qn - nq):
+        // disjoint when nq = 64, and the whole queue when nq = qn)
+        const int rest = qn - nq;
+        uint32_t k2 = 0;
+        int64_t t2 = 0;
+        if (lane < rest) {
+            k2 = qk[w][nq + lane];
+            if constexpr (MODE >= 2) t2 = qt[w][nq + lane];
+        }
+        if (lane < rest) {
+            qk[w][lane] = k2;
+            if constexpr (MODE >= 2) qt[w][lane] = t2;
+        }
+        qn = rest;
+    };
     // this lane's event of the next chunk, loaded one chunk ahead
     int nv = 0;
     int64_t nt = 0;
@@ -317,39 +381,39 @@ __global__ __launch_bounds__(64 * kFsWaves) void frame_series_kernel(
         }
 #pragma unroll
         for (int q = 0; q < kFrameWords; ++q) t[q] = wave_xscan64(t[q]) ^ m[q];
-        double sl = 0.0, an = 0.0;
-        int cnt = 0;
-        if (i < ne) frame_eval(t, md, cx, cy, sl, an, cnt);
         if constexpr (MODE == 0) {
+            double sl = 0.0, an = 0.0;
+            int cnt = 0;
             if (i < ne) {
+                frame_eval(t, md, cx, cy, sl, an, cnt);
                 so[i + 1] = sl;
                 ao[i + 1] = an;
                 co[i + 1] = cnt;
             }
         } else {
-            const uint64_t bs = (uint64_t)__double_as_longlong(sl), ba = (uint64_t)__double_as_longlong(an);
-            uint64_t ps = shfl_up64(bs, 1), pa = shfl_up64(ba, 1);
-            if (lane == 0) {
-                ps = prev_s;
-                pa = prev_a;
+            // only an event whose key differs from the previous event's can change the values: those
+            // events are queued (in order) and evaluated 64 at a time
+            int cnt;
+            const uint32_t key = i < ne ? frame_key(t, cnt) : kNoPair;
+            uint32_t pk = (uint32_t)__shfl_up((int)key, 1);
+            if (lane == 0) pk = prev_key;
+            const bool cand = i < ne && key != pk;
+            const uint64_t qm = __ballot(cand);
+            if (cand) {
+                const int qi = qn + __popcll(qm & ((1ull << lane) - 1ull));
+                qk[w][qi] = key;
+                if constexpr (MODE >= 2) qt[w][qi] = tcur;
             }
-            const bool chg = i < ne && (bs != ps || ba != pa);
-            const uint64_t cmk = __ballot(chg);
-            if constexpr (MODE >= 2) {
-                if (chg) {
-                    const int64_t o = pos + __popcll(cmk & ((1ull << lane) - 1ull));
-                    so[o] = sl;
-                    ao[o] = an;
-                    to[o] = tcur;
-                }
-            }
-            pos += __popcll(cmk);
+            qn += __popcll(qm);
             const int last = (int)((ne - b < 64 ? ne - b : 64) - 1);  // the chunk's last event
-            prev_s = (uint64_t)__shfl((long long)bs, last);
-            prev_a = (uint64_t)__shfl((long long)ba, last);
+            prev_key = (uint32_t)__shfl((int)key, last);
+            if (qn >= 64) flush(64);
         }
 #pragma unroll
         for (int q = 0; q < kFrameWords; ++q) m[q] = (uint64_t)__shfl((long long)t[q], 63);
+    }
+    if constexpr (MODE >= 1) {
+        if (qn > 0) flush(qn);
     }
     if constexpr (MODE == 1 || MODE == 3) {
         if (lane == 0) {
