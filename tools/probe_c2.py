@@ -18,6 +18,7 @@ bases = np.asarray([G.SEC11_BASES[c % 10 if B < 0 else B] for c in range(C)])
 cfg = RunConfig(seed=0x5EED0002, pop_lo=lo, pop_hi=hi, tune=parse_tune(os.environ.get('FC_TUNE', '')),
                 stream=os.environ.get('FC_STREAM', 'node'))
 if 'FC_PROBE_DIAG' in os.environ: cfg.diag_mask = int(os.environ['FC_PROBE_DIAG'])
+if 'FC_PROBE_EVCAP' in os.environ: cfg.event_cap = int(os.environ['FC_PROBE_EVCAP'])  # FC_DIAG_SERIES event log
 run = FlipRun(fg, inits, cfg, bases=bases)
 for it in range(IT):
     s0 = run.stats()
