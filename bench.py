@@ -494,7 +494,7 @@ def c_oracle_allcores(seconds: float, cores: int, wname: str = "c2"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=40)  # 40 launches: ~2 s of timed GPU work per run
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chain-steps", type=int, default=100000)
     ap.add_argument("--chains", type=int, default=0, help="chains per GPU (0: the workload's)")
