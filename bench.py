@@ -504,7 +504,7 @@ def main():
     ap.add_argument("--sweep-replicas", type=int, default=1,
                     help="side line (N = 1, c2): the reference's two sweeps -- all 174 configurations x R replicas, "
                          "100,000 yields each, every output file written (flipcomplexityempirical_amd.sweep); 0: skip")
-    ap.add_argument("--full-diag-steps", type=int, default=3,
+    ap.add_argument("--full-diag-steps", type=int, default=6,
                     help="launches of the full-diagnostics side line (0: skip)")
     ap.add_argument("--acf-yields", type=int, default=10 * 65536,
                     help="C4 diagnostics leg: yields of the one series window the autocorrelation covers "
@@ -676,7 +676,8 @@ def main():
         lags = [1 << i for i in range(17)]
         rf = FlipRun(fg, inits, cfg_f, bases=bases)
         frame = G.slope_frame(spec, "sec11") if series else None
-        rf.steps(args.chain_steps)
+        for _ in range(max(1, args.warmup)):  # untimed, as the headline leg's warmup launches
+            rf.steps(args.chain_steps)
         barrier_sync_f = lambda: (rf.sync(), dist.barrier() if dist is not None else None)  # noqa: E731
         cp_buf = None
         if series:

@@ -348,22 +348,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
     // a store only some lanes make: the others write the sink (no branch; storing under exec
     // masks instead measured no faster, profiles/r03c_ab_masked_stores)
 #define FC_ST(cond, ref, val) (*((cond) ? (uint8_t *)&(ref) : dum) = (uint8_t)(val))
-#ifdef FC_EXP_DUP  // bank-conflict attribution builds (timing-only): one LDS access kind issued twice
-#define FC_DUPR(K, ref)                                                    \
-    do {                                                                   \
-        if (FC_EXP_DUP == (K)) {                                           \
-            const int x_ = *(volatile const uint8_t *)&(ref);              \
-            asm volatile("" ::"v"(x_));                                    \
-        }                                                                  \
-    } while (0)
-#define FC_DUPS(K, cond, ref, val)                                                             \
-    do {                                                                                       \
-        if (FC_EXP_DUP == (K)) *(volatile uint8_t *)((cond) ? (uint8_t *)&(ref) : dum) = (uint8_t)(val); \
-    } while (0)
-#else
-#define FC_DUPR(K, ref) do {} while (0)
-#define FC_DUPS(K, cond, ref, val) do {} while (0)
-#endif
     // accepted states whose geometric wait is still to be drawn (kWaitQ of them:
     // creating draw, |B| after the flip, yields so far); see wait_flush below
     uint64_t *q_d = (uint64_t *)(nmark + npad + 16);
@@ -621,7 +605,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 // (vdj < n on every lane: the read needs no guard)
                 okm |= (uint32_t)ok << j;
                 hb |= (uint32_t)(ok & (fcnt[vdj[j]] != 0)) << j;
-                FC_DUPR(1, fcnt[vdj[j]]);
             }
             const int hc = __popc(hb);
             const int incl = wave_scan_incl(hc);
@@ -751,7 +734,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         for (int i = 0; i < RMAX; ++i) {
             cell[i] = ring_entry<RMAX>(rec.ring, i);
             ad[i] = a[cell[i]];
-            FC_DUPR(2, a[cell[i]]);
         }
         // every read issued before the first use (the compiler otherwise waited on each read
         // before issuing the next: eight LDS round trips in a row)
@@ -934,7 +916,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
 #pragma unroll
                         for (int i = 0; i < RMAX; ++i) {
                             const int oc = fcnt[cell[i]];
-                            FC_DUPR(4, fcnt[cell[i]]);
                             const bool nb_i = (nbr >> i) & 1u;
                             dnb_l += nb_i ? (int)(((inA >> i) & 1u) && oc == 0) - (int)(((tmask >> i) & 1u) && oc == 1) : 0;
                         }
@@ -1009,18 +990,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         FC_ST(need && ms > lane, smark[v], lane);
                         const uint32_t wm = need ? (nbr & gtm) : 0u;
 #pragma unroll
-                        for (int i = 0; i < RMAX; ++i) {
-                            FC_ST((wm >> i) & 1u, nmark[cell[i]], lane);
-                            FC_DUPS(5, (wm >> i) & 1u, nmark[cell[i]], lane);
-                        }
+                        for (int i = 0; i < RMAX; ++i) FC_ST((wm >> i) & 1u, nmark[cell[i]], lane);
                         compiler_fence();
                         ms = smark[v];
                         int mn[RMAX];
 #pragma unroll
-                        for (int i = 0; i < RMAX; ++i) {
-                            mn[i] = nmark[cell[i]];
-                            FC_DUPR(3, nmark[cell[i]]);
-                        }
+                        for (int i = 0; i < RMAX; ++i) mn[i] = nmark[cell[i]];
 #pragma unroll
                         for (int r = 0; r < kRV; ++r) mk[r] = nmark[rv[r] < 0 ? 0 : (rv[r] & 0xffff)];
                         gtm = 0u;
@@ -1040,10 +1015,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     // neighbour shared with an earlier candidate
                     bool conf = (ms < lane) | (inK & ((nbr & ltm) != 0u));
 #pragma unroll
-                    for (int i = 0; i < RMAX; ++i) {
-                        conf |= (int)smark[cell[i]] < lane;
-                        FC_DUPR(3, smark[cell[i]]);
-                    }
+                    for (int i = 0; i < RMAX; ++i) conf |= (int)smark[cell[i]] < lane;
                     conf &= has;
                     const uint64_t XX = __ballot(conf && lane > pos && lane < end);
                     if (XX) {
@@ -1109,10 +1081,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                     // in t); beta leaves every u to one flip of the segment
                     int oldc[RMAX];
 #pragma unroll
-                    for (int i = 0; i < RMAX; ++i) {
-                        oldc[i] = fcnt[cell[i]];
-                        FC_DUPR(4, fcnt[cell[i]]);
-                    }
+                    for (int i = 0; i < RMAX; ++i) oldc[i] = fcnt[cell[i]];
                     compiler_fence();
                     int dnb = 0;
                     // (bit masks, not short-circuit tests: those compiled to a branch per cell)
@@ -1124,7 +1093,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                         const int nw = oldc[i] + 2 * (int)((inA >> i) & 1u) - 1;
                         const uint32_t nb_i = (nbm >> i) & 1u;
                         FC_ST(nb_i, fcnt[cell[i]], nw);
-                        FC_DUPS(6, nb_i, fcnt[cell[i]], nw);
                         dnb += (min(nw, 1) - min(oldc[i], 1)) & -(int)nb_i;
                     }
                     FC_ST(me, *(uint8_t *)&a[v], 1 - av);

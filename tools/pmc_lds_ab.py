@@ -1,6 +1,6 @@
 """Per-library LDS / issue counters of tools/pmc_lds_ab.sh: the flip-kernel dispatches after the
 first (warm-up) one, averaged; each variant's difference to the first library (the base).  A
-variant that issues one LDS access kind twice (fc_flip2.hip FC_EXP_DUP) adds that kind's own
+variant that issues one LDS access kind twice (tools/patches/lds_dup_attribution.patch, -DFC_EXP_DUP=k) adds that kind's own
 instructions, array cycles and bank-conflict cycles once more, so its difference attributes them."""
 import csv
 import glob
