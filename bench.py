@@ -676,7 +676,10 @@ def main():
         lags = [1 << i for i in range(17)]
         rf = FlipRun(fg, inits, cfg_f, bases=bases)
         frame = G.slope_frame(spec, "sec11") if series else None
-        for _ in range(max(1, args.warmup)):  # untimed, as the headline leg's warmup launches
+        n_wu = max(1, args.warmup)
+        for i in range(n_wu):  # untimed, as the headline leg's warmup launches
+            if i and (series or c4diag):
+                rf.series_reset()  # (the event log holds one window; the last warmup's sizes the buffers)
             rf.steps(args.chain_steps)
         barrier_sync_f = lambda: (rf.sync(), dist.barrier() if dist is not None else None)  # noqa: E731
         cp_buf = None
