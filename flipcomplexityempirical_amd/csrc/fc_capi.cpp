@@ -1624,7 +1624,7 @@ int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_fra
     const int64_t sub = 64 * ((nk + fc::kFrameWaves - 1) / fc::kFrameWaves) + 1;
     const int64_t stage_cap = sub * fc::kFrameWaves;
     bool staged = false;
-    if (!query) {
+    if (!query && !(r->p.flags & FC_FLAG_SERIES_TWO_PASS)) {
         const size_t want = (size_t)r->n_chains * (size_t)stage_cap;
         if (want > r->fc_stage_cap) {
             size_t free_b = 0, total_b = 0;

@@ -84,6 +84,10 @@ extern "C" {
 
 /* fc_params.flags */
 #define FC_FLAG_FORCE_BFS 0x1u   /* resolve every multi-run contiguity case by device BFS   */
+#define FC_FLAG_SERIES_TWO_PASS 0x2u /* fc_run_frame_series_changes: the two-pass form (count, then
+                                    write at the offsets) instead of one staged pass -- the form a
+                                    run whose staging exceeds a tenth of free device memory takes;
+                                    same output (a cross-check)                                 */
 
 typedef struct fc_graph fc_graph;
 typedef struct fc_run fc_run;

@@ -29,12 +29,12 @@ pytestmark = pytest.mark.gpu
 ANGLE_TOL = 1e-6
 
 
-def _run(spec, plans, bases, pct, seed=5):
+def _run(spec, plans, bases, pct, seed=5, flags=0):
     fg = FlipGraph(spec)
     _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), 2, pct)
     inits = np.stack([spec.assignment_array(p, [-1, 1]) for p in plans])
     cfg = RunConfig(seed=seed, pop_lo=lo, pop_hi=hi, diag_mask=_lib.FC_DIAG_WAIT | _lib.FC_DIAG_SERIES,
-                    event_cap=100000)
+                    event_cap=100000, flags=flags)
     return FlipRun(fg, inits, cfg, bases=np.asarray(bases, dtype=np.float64)), inits
 
 
@@ -189,3 +189,27 @@ def test_frame_series_changes_equal_per_yield_lists(gpu, sec11, launches):
     lo, hi = int(full["offsets"][2]), int(full["offsets"][7])
     for key in ("t", "slope", "angle"):
         assert np.array_equal(full[key][lo:hi].view(np.int64), ch[key].view(np.int64)), key
+
+
+def test_frame_series_changes_two_pass_form_equals_staged(gpu, sec11):
+    """The two forms of fc_run_frame_series_changes -- one staged pass (count and write into
+    per-wave ranges, then packed) and the two-pass count / write form a run falls back to when the
+    staging does not fit (FC_FLAG_SERIES_TWO_PASS) -- give the same change points, bit for bit,
+    over windows of one and of several launches, on a chunk of chains not starting at 0."""
+    bases = [0.1, 0.8, 1.0, G.SEC11_MU, 10.0, 0.3, 4.0, 2.0] * 8
+    plans = [G.sec11_plan(c % 3, sec11.nodes) for c in range(len(bases))]
+    a, _ = _run(sec11, plans, bases, 0.1)
+    b, _ = _run(sec11, plans, bases, 0.1, flags=_lib.FC_FLAG_SERIES_TWO_PASS)
+    frame = G.slope_frame(sec11, "sec11")
+    for launches in (1, 3):
+        for r in (a, b):
+            r.series_reset()
+            for _ in range(launches):
+                r.steps(2000)
+        x = a.frame_series_changes(frame, c0=3, nc=50)
+        y = b.frame_series_changes(frame, c0=3, nc=50)
+        assert np.array_equal(x["offsets"], y["offsets"])
+        assert x["offsets"][-1] > 50
+        assert np.array_equal(x["t"], y["t"])
+        for key in ("slope", "angle"):
+            assert np.array_equal(x[key].view(np.int64), y[key].view(np.int64)), key
