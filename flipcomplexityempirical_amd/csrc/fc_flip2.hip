@@ -766,6 +766,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         uint32_t st = (hit ? LF_HIT : 0u) | (acc ? LF_ACC : 0u) | (s_lin ? LF_SLIN : 0u) | (s_cyc ? LF_SCYC : 0u) |
                       (exact ? LF_EXACT : 0u) | (gam ? LF_GAM : 0u) | (has ? LF_HAS : 0u);
         if (XTRA && (rec.meta & kMetaFrozen)) st |= LF_FRZ;
+#ifdef FC_PHASE_PROF
+        bool first_it = true;
+#endif
         FC_STAMP(t_c);
         FC_PROF(2, t_c - t_b);
 
@@ -866,6 +869,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
         while (pos < end) {
             FC_PROF(6, 1);
             FC_STAMP(t_it0);
+#ifdef FC_PHASE_PROF
+            if (first_it) FC_PROF(27, t_it0 - t_c);  // the commit's set-up
+            first_it = false;
+#endif
             // re-derive the predicates each iteration: loop-invariant lane values would otherwise
             // be hoisted as lane masks into SGPRs and spilled
             asm volatile("" : "+v"(st), "+v"(inA), "+v"(tmask), "+v"(nbr), "+v"(delta), "+v"(nA), "+v"(av), "+v"(pv),
@@ -1139,12 +1146,16 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 if (pos >= end) break;
                 if (stale_seg && AP) {  // a committed flip changed the view of a later slot
                     reeval(pos, -1, 0u);
+                    FC_STAMP(t_sg2);
+                    FC_PROF(29, t_sg2 - t_sg1);
                     continue;
                 }
                 if (SEARCH && u == pos) {
                     const bool res = run_bfs(u);
                     if (lane == u) st |= ST_BD | (res ? ST_BR : 0u);
                 }
+                FC_STAMP(t_sg3);
+                FC_PROF(29, t_sg3 - t_sg1);
                 continue;
             }
             // ---- one event at a time: the first acceptance or undecided lane -----------------
@@ -1165,7 +1176,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
             st |= (prop & (lane < f)) ? bits : 0u;
             rem -= nvalid;
             pos = f;
-            if (f >= end) break;
+            if (f >= end) {
+                FC_STAMP(t_fx);
+                FC_PROF(25, t_fx - t_it1);  // the last iteration: no event left
+                break;
+            }
             if (SEARCH && !((VAL >> f) & 1ull)) {
                 const bool res = run_bfs(f);
                 if (lane == f) st |= ST_BD | (res ? ST_BR : 0u);
@@ -1271,6 +1286,8 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? 4 : 1)) void flip2_kernel(KParams
                 break;
             }
             if (aff && pos < end) reeval(pos, vf, eqm);
+            FC_STAMP(t_ap2);
+            FC_PROF(30, t_ap2 - t_ap1);
         }
         compiler_fence();  // (the marks: cleared by each segment pass)
         steps = steps0 + (rem0 - rem);

@@ -42,6 +42,13 @@ if S >= 28:
         x = last[np.arange(C) % G == g].mean(axis=0)
         b = max(x[5], 1)
         print(f"{g:3d} | {x[24]/b:6.2f} {x[22]/b:6.3f} {x[23]/max(x[22],1):8.0f}")
+if S >= 32:
+    print("grp | per batch: commit set-up, last no-event iteration, after a segment pass (incl. reeval), after a one-event apply (incl. reeval) | commit left")
+    for g in range(G):
+        x = last[np.arange(C) % G == g].mean(axis=0)
+        b = max(x[5], 1)
+        known = x[8] + x[9] + x[10] + x[11] + x[25] + x[27] + x[29] + x[30]
+        print(f"{g:3d} | {x[27]/b:8.0f} {x[25]/b:8.0f} {x[29]/b:8.0f} {x[30]/b:8.0f} | {(x[3]-known)/b:8.0f}")
 print("max chain total Mcyc", last[:, 0].max() / 1e6, "argmax", int(last[:, 0].argmax()))
 tot = last[:, 0]
 print("per group total Mcyc mean / p90 / max:",
