@@ -24,6 +24,7 @@ exits with the first failing rank's status.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -833,16 +834,21 @@ def main():
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     acc_pp = per_launch_acc / per_launch_props if per_launch_props else 0.0
     lds_peak = lds_mix_peak_gbs(W.rmix, W.wmix, acc_pp)
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tfile):
+    traffic, traffic_src = None, None
+    # HBM bytes per launch from the separate FETCH_SIZE / WRITE_SIZE passes of the same kernel
+    # and run shape: profiles/pmc_traffic.json (C2), the newest profiles/*_side_pmc_<w>.json (k > 2)
+    tfiles = [os.path.join(ROOT, "profiles", "pmc_traffic.json")] if args.workload == "c2" else \
+        sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_side_pmc_{args.workload}.json")), reverse=True)
+    for tfile in tfiles:
         try:
             tj = json.load(open(tfile))
             if (tj.get("chains") == C and tj.get("chain_steps") == args.chain_steps
-                    and tj.get("workload", "c2") == args.workload and kname in str(tj.get("kernel"))):
-                traffic = tj.get("hbm_bytes_per_launch")
+                    and tj.get("workload", "c2") == args.workload and kname in str(tj.get("kernel"))
+                    and tj.get("hbm_bytes_per_launch")):
+                traffic, traffic_src = tj["hbm_bytes_per_launch"], "profiles/" + os.path.basename(tfile)
+                break
         except Exception:
-            traffic = None
+            continue
     levels = roofline_levels(W, per_launch_props, per_launch_acc, kernel_ms, traffic)
     l1l2 = measured_l2(args.workload, kname, C, args.chain_steps, kernel_ms, _lib.build_id())
     out = {
@@ -889,8 +895,9 @@ def main():
                                   "mix (MI355X_MICROARCH.md §LDS: u8 / u16 / b32 reads 32 / 64 / 128 B/clk/CU, writes "
                                   "half; 256 CUs, 2.4 GHz; reads %s B, writes %s B per accept, %.3f accepts per "
                                   "proposal), the round-3 pricing" % (W.rmix, W.wmix, acc_pp),
-                     "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE "
-                                     "(profiles/pmc_traffic.json; gfx950 FETCH_SIZE doubled)",
+                     "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of "
+                                     "this kernel and run shape (%s; gfx950 FETCH_SIZE doubled)"
+                                     % (traffic_src or "none recorded for it"),
                      "kernel": kname,
                      "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": alg_bytes,

@@ -23,8 +23,9 @@ for w in c3 c4 c5; do
   timeout -k 10 300 python3 bench.py --workload $w --steps 5 --warmup 1 --chain-steps 20000 --no-cpu-baseline --full-diag-steps $FD > "$OUT/side_$w.json" 2> "$OUT/side_$w.err" || { echo "side $w failed"; tail -20 "$OUT/side_$w.err"; exit 1; }
   cat "$OUT/side_$w.json"
 done
-# counters of the k > 2 instances (C4 flip_kernel<8,2,3,false>, C5 flip_kernel<16,4,3,false>)
-for w in c4 c5; do
+# counters of the k > 2 instances (C3 flip_kernel<8,2,3,false,2>, C4 flip_kernel<8,2,3,false,1>,
+# C5 flip_kernel<16,4,3,false,1>)
+for w in ${SIDE_PMC:-c3 c4 c5}; do
   SB="bench.py --workload $w --steps 2 --warmup 1 --chain-steps 20000 --no-cpu-baseline --full-diag-steps 0"
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $C -d "$OUT/side_pmc_${w}_$C" -o pmc --output-format csv -- python3 $SB > "$OUT/side_pmc_${w}_$C.log" 2>&1 || { echo "side pmc $w $C failed"; tail -20 "$OUT/side_pmc_${w}_$C.log"; exit 1; }

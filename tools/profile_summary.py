@@ -117,11 +117,17 @@ for w in ("c3", "c4", "c5"):
     if os.path.exists(p):
         line = json.loads(open(p).read().strip().splitlines()[-1])
         json.dump(line, open(os.path.join(dst, f"{tag}_side_{w}.json"), "w"), indent=1)
-for w in ("c4", "c5"):  # counters of the k > 2 instances
+for w in ("c3", "c4", "c5"):  # counters of the k > 2 instances
     d = os.path.join(src, f"side_pmc_{w}_lds", "pmc_counter_collection.csv")
     if not os.path.exists(d):
         continue
     side = lds_issue(d, "fc::flip_kernel")
+    # the run they come from (tools/gpu_profile.sh: 20,000-step launches of the side line's
+    # resident chains), which bench.py matches before it reports them as the line's traffic
+    side["chain_steps"] = 20000
+    p = os.path.join(src, f"side_{w}.json")
+    if os.path.exists(p):
+        side["chains"] = json.loads(open(p).read().strip().splitlines()[-1])["config"]["chains_per_gpu"]
     hb = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         rows = [r for r in flip_rows(os.path.join(src, f"side_pmc_{w}_{c}", "pmc_counter_collection.csv"))
