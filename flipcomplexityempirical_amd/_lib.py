@@ -28,6 +28,7 @@ FC_DIAG_WAIT, FC_DIAG_HIST, FC_DIAG_EDGES, FC_DIAG_FLIPS, FC_DIAG_SERIES = 0x1, 
 FC_DIAG_FLIPS_EXACT = 0x20
 FC_FLAG_FORCE_BFS = 0x1
 FC_FLAG_SERIES_TWO_PASS = 0x2  # fc_run_frame_series_changes' two-pass form (cross-check)
+FC_FLAG_TALLY_LOG_SMALL = 0x4  # a 64-entry tally log: the overflow path's atomics (cross-check)
 FC_ACCEPT_CUT, FC_ACCEPT_UNIFORM, FC_ACCEPT_ANNEAL = 0, 1, 2
 FC_CON_CONTIG, FC_CON_POP, FC_CON_BOUNDARY, FC_CON_FIXED, FC_CON_EMPTY = 0x1, 0x2, 0x4, 0x8, 0x100
 

@@ -980,6 +980,7 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
         chunk = int64_t(1) << 23;
         const int64_t steps1 = std::min(chunk, n_steps);
         int64_t want = steps1 + steps1 / 8 + 256;
+        if (r->p.flags & FC_FLAG_TALLY_LOG_SMALL) want = std::min<int64_t>(want, 64);
         if (want > r->tl_cap) {
             size_t free_b = 0, total_b = 0;
             HIP_TRY(hipMemGetInfo(&free_b, &total_b));

@@ -88,6 +88,10 @@ extern "C" {
                                     write at the offsets) instead of one staged pass -- the form a
                                     run whose staging exceeds a tenth of free device memory takes;
                                     same output (a cross-check)                                 */
+#define FC_FLAG_TALLY_LOG_SMALL 0x4u /* k = 2 full diagnostics: a 64-entry tally log per chain, so
+                                    chains fill it and apply the rest of a launch's tallies with
+                                    atomics -- the path a device short of memory takes; same
+                                    output (a cross-check)                                      */
 
 typedef struct fc_graph fc_graph;
 typedef struct fc_run fc_run;
