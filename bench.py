@@ -217,6 +217,26 @@ def resident_chains(fg, W, device: int = 0, flags: int = 0, tune=None) -> int:
     return cus * max(1, min(160 * 1024 // lds, 16))
 
 
+def measured_traffic(wname: str, kname: str, chains: int, chain_steps: int, root: str = ROOT):
+    """HBM bytes per launch of this kernel at this launch shape, from the separate rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md HBM section: (2 FETCH_SIZE + WRITE_SIZE)
+    KiB): profiles/pmc_traffic.json for C2, the newest profiles/r*_side_pmc_<workload>.json for the
+    k > 2 side lines.  Returns (bytes, profile) or (None, None) when none matches."""
+    prof = os.path.join(root, "profiles")
+    files = [os.path.join(prof, "pmc_traffic.json")] if wname == "c2" else \
+        sorted(glob.glob(os.path.join(prof, f"r*_side_pmc_{wname}.json")), reverse=True)
+    for fn in files:
+        try:
+            tj = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        if (tj.get("chains") == chains and tj.get("chain_steps") == chain_steps
+                and tj.get("workload", "c2") == wname and kname in str(tj.get("kernel"))
+                and tj.get("hbm_bytes_per_launch")):
+            return tj["hbm_bytes_per_launch"], "profiles/" + os.path.basename(fn)
+    return None, None
+
+
 def measured_l2(wname: str, kname: str, chains: int, chain_steps: int, kernel_ms: float, build_id: str = ""):
     """The newest committed L1 / L2 counter summary of this workload's kernel at this launch shape
     (profiles/*_<workload>_l1l2.json, tools/gpu_cache_pmc.sh), rescaled to this run's launch time:
@@ -834,21 +854,7 @@ def main():
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     acc_pp = per_launch_acc / per_launch_props if per_launch_props else 0.0
     lds_peak = lds_mix_peak_gbs(W.rmix, W.wmix, acc_pp)
-    traffic, traffic_src = None, None
-    # HBM bytes per launch from the separate FETCH_SIZE / WRITE_SIZE passes of the same kernel
-    # and run shape: profiles/pmc_traffic.json (C2), the newest profiles/*_side_pmc_<w>.json (k > 2)
-    tfiles = [os.path.join(ROOT, "profiles", "pmc_traffic.json")] if args.workload == "c2" else \
-        sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_side_pmc_{args.workload}.json")), reverse=True)
-    for tfile in tfiles:
-        try:
-            tj = json.load(open(tfile))
-            if (tj.get("chains") == C and tj.get("chain_steps") == args.chain_steps
-                    and tj.get("workload", "c2") == args.workload and kname in str(tj.get("kernel"))
-                    and tj.get("hbm_bytes_per_launch")):
-                traffic, traffic_src = tj["hbm_bytes_per_launch"], "profiles/" + os.path.basename(tfile)
-                break
-        except Exception:
-            continue
+    traffic, traffic_src = measured_traffic(args.workload, kname, C, args.chain_steps)
     levels = roofline_levels(W, per_launch_props, per_launch_acc, kernel_ms, traffic)
     l1l2 = measured_l2(args.workload, kname, C, args.chain_steps, kernel_ms, _lib.build_id())
     out = {
