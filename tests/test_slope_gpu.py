@@ -213,3 +213,41 @@ def test_frame_series_changes_two_pass_form_equals_staged(gpu, sec11):
         assert np.array_equal(x["t"], y["t"])
         for key in ("slope", "angle"):
             assert np.array_equal(x[key].view(np.int64), y[key].view(np.int64)), key
+
+
+def test_frame_series_changes_at_full_c2_size(gpu, sec11):
+    """At BASELINE config C2's size (4096 chains, one 100,000-step launch, ~165 M events) the
+    change points of a sample of chains spread over the run are exactly the per-event series'
+    entries whose (slope, angle) bits differ from the previous entry's, at the events' yields
+    (window start first) -- a size-independent property of the two device forms."""
+    C = 4096
+    bases = [G.SEC11_BASES[c % 10] for c in range(C)]
+    plans = [G.sec11_plan((c // 10) % 3, sec11.nodes) for c in range(C)]
+    fg = FlipGraph(sec11)
+    _, (lo, hi) = G.population_bounds(int(sec11.pop.sum()), 2, 0.1)
+    inits = np.stack([sec11.assignment_array(p, [-1, 1]) for p in plans])
+    cfg = RunConfig(seed=0x5EED0002, pop_lo=lo, pop_hi=hi, diag_mask=_lib.FC_DIAG_WAIT | _lib.FC_DIAG_SERIES,
+                    event_cap=100001)
+    run = FlipRun(fg, inits, cfg, bases=np.asarray(bases, dtype=np.float64))
+    run.steps(100000)
+    frame = G.slope_frame(sec11, "sec11")
+    ch = run.frame_series_changes(frame)
+    st = run.stats()
+    assert ch["offsets"][-1] < int(st["events"].sum())
+    sample = list(range(0, C, 97)) + [C - 1]
+    for c0 in range(0, len(sample), 16):
+        cs = sample[c0:c0 + 16]
+        for c in cs:
+            dense = run.frame_series(frame, chains=[c])
+            n = int(dense["len"][0])
+            s = dense["slope"][0, :n].view(np.int64)
+            a = dense["angle"][0, :n].view(np.int64)
+            keep = np.ones(n, dtype=bool)
+            keep[1:] = (s[1:] != s[:-1]) | (a[1:] != a[:-1])
+            ev_t = run.events(c)["t"].astype(np.int64)
+            t_all = np.concatenate([[int(st["series_t0"][c])], ev_t])
+            lo_, hi_ = int(ch["offsets"][c]), int(ch["offsets"][c + 1])
+            assert hi_ - lo_ == int(keep.sum()), c
+            assert np.array_equal(ch["t"][lo_:hi_], t_all[keep]), c
+            assert np.array_equal(ch["slope"][lo_:hi_].view(np.int64), s[keep]), c
+            assert np.array_equal(ch["angle"][lo_:hi_].view(np.int64), a[keep]), c
