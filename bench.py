@@ -374,17 +374,50 @@ def _dist():
     return dist, dist.get_rank(), dist.get_world_size(), local
 
 
+def device_identity(local: int) -> str:
+    """This rank's device: the PCI bus id of HIP device ``local`` (fc_device_pci_id), or, with no
+    GPU (the CPU launcher test), ``cpu:<host>:<pid>``."""
+    import socket
+    try:
+        from flipcomplexityempirical_amd import _lib
+        if _lib.device_count() > 0:
+            import ctypes
+            buf = ctypes.create_string_buffer(32)
+            if _lib.load().fc_device_pci_id(int(local), buf, 32) == 0:
+                return buf.value.decode()
+    except Exception:  # no library / no device: the CPU identity below
+        pass
+    return f"cpu:{socket.gethostname()}:{os.getpid()}"
+
+
+def gather_devices(dist, local: int) -> dict:
+    """Every rank's device identity, gathered on all ranks (an N-GPU line shows
+    that N distinct GPUs did the work).  ``distinct`` is False only in rehearsals that put several
+    ranks on one device (FC_BENCH_DEVICE)."""
+    me = {"rank": dist.get_rank() if dist is not None else 0, "local_rank": local,
+          "device": device_identity(local), "host": __import__("socket").gethostname()}
+    if dist is None:
+        ids = [me]
+    else:
+        ids = [None] * dist.get_world_size()
+        dist.all_gather_object(ids, me)
+    keys = [(d["host"], d["device"]) for d in ids]
+    return {"per_rank": ids, "distinct": len(set(keys)) == len(keys)}
+
+
 def spawn_probe():
     """FC_BENCH_SPAWN_PROBE=1 (CPU test of the launcher, tests/test_bench_launch.py): each rank
-    joins the process group over gloo, sums its rank, and rank 0 prints what it saw."""
+    joins the process group over gloo, sums its rank, gathers every rank's device identity, and
+    rank 0 prints what it saw."""
     import torch
     import torch.distributed as dist
     dist.init_process_group(backend="gloo")
     t = torch.tensor([float(dist.get_rank())])
     dist.all_reduce(t)
+    devs = gather_devices(dist, int(os.environ.get("LOCAL_RANK", "0")))
     if dist.get_rank() == 0:
         print(json.dumps({"ranks_seen": dist.get_world_size(), "rank_sum": float(t.item()),
-                          "launcher": os.environ.get("FC_BENCH_LAUNCHER", "external")}), flush=True)
+                          "launcher": os.environ.get("FC_BENCH_LAUNCHER", "external"), "devices": devs}), flush=True)
     dist.destroy_process_group()
 
 
@@ -630,6 +663,11 @@ def main():
     elapsed = D.allreduce_max(elapsed, dist, dev)
     kernel_ms = D.allreduce_max(kernel_ms, dist, dev)
     props, steps, acc = (float(agg[:, D.AGG_FIELDS.index(k)].sum()) for k in ("proposals", "steps", "accepted"))
+    # every rank's device (PCI bus id): an N-GPU line must show N distinct GPUs; only a rehearsal
+    # (FC_BENCH_DEVICE: several ranks on one device) may share one
+    devices = gather_devices(dist, local_rank)
+    if world > 1 and not devices["distinct"] and "FC_BENCH_DEVICE" not in os.environ:
+        raise SystemExit(f"bench.py: ranks share a device: {devices['per_rank']}")
 
     node_out = None
     if stream == "band" and args.node_stream_steps > 0:
@@ -865,6 +903,7 @@ def main():
         "ranks_seen": dist.get_world_size() if dist is not None else 1,
         "backend": dist.get_backend() if dist is not None else None,
         "launcher": os.environ.get("FC_BENCH_LAUNCHER") or ("torch.distributed.run" if dist is not None else None),
+        "devices": devices,
         "per_rank_kernel_ms": [float(x) for x in rank_rec[0]],
         "per_rank_elapsed_s": [float(x) for x in rank_rec[1]],
         "build_flags": _lib.build_flags(),

@@ -29,6 +29,7 @@ FC_DIAG_FLIPS_EXACT = 0x20
 FC_FLAG_FORCE_BFS = 0x1
 FC_FLAG_SERIES_TWO_PASS = 0x2  # fc_run_frame_series_changes' two-pass form (cross-check)
 FC_FLAG_TALLY_LOG_SMALL = 0x4  # a 64-entry tally log: the overflow path's atomics (cross-check)
+FC_FLAG_NB_PAIRS = 0x8  # k > 2: |b_nodes| counts the pair updater's (node, district) pairs (:151-153)
 FC_ACCEPT_CUT, FC_ACCEPT_UNIFORM, FC_ACCEPT_ANNEAL = 0, 1, 2
 FC_CON_CONTIG, FC_CON_POP, FC_CON_BOUNDARY, FC_CON_FIXED, FC_CON_EMPTY = 0x1, 0x2, 0x4, 0x8, 0x100
 
@@ -40,8 +41,8 @@ EXPORTED = [
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_flips_exact", "fc_run_read_wait_expected",
     "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
     "fc_run_frame_series", "fc_run_frame_series_changes", "fc_host_register", "fc_host_unregister",
-    "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_destroy",
-    "fc_device_count", "fc_last_error", "fc_build_flags", "fc_build_id",
+    "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_nb_width", "fc_run_destroy",
+    "fc_device_count", "fc_device_pci_id", "fc_last_error", "fc_build_flags", "fc_build_id",
 ]
 
 FC_BUILD_PHASE_PROF, FC_BUILD_PHASE_SYNC, FC_BUILD_VARIANT = 0x1, 0x2, 0x4  # include/flipchain.h
@@ -213,6 +214,9 @@ def load(build_if_missing: bool = True, allow_variant: bool = False):
     L.fc_run_n_chains.restype = i32
     L.fc_run_chain_lds_bytes.argtypes = [vp]
     L.fc_run_chain_lds_bytes.restype = i32
+    L.fc_run_nb_width.argtypes = [vp]
+    L.fc_run_nb_width.restype = i32
+    L.fc_device_pci_id.argtypes = [i32, ctypes.c_char_p, i32]
     L.fc_run_destroy.argtypes = [vp]
     L.fc_run_destroy.restype = None
     L.fc_device_count.argtypes = [_P(i32)]
@@ -224,7 +228,7 @@ def load(build_if_missing: bool = True, allow_variant: bool = False):
     L.fc_build_id.restype = ctypes.c_char_p
     for name in EXPORTED:
         if name not in ("fc_graph_destroy", "fc_run_destroy", "fc_last_error", "fc_run_n_chains",
-                        "fc_run_chain_lds_bytes", "fc_build_flags", "fc_build_id"):
+                        "fc_run_chain_lds_bytes", "fc_run_nb_width", "fc_build_flags", "fc_build_id"):
             getattr(L, name).restype = ctypes.c_int
     bf = int(L.fc_build_flags())
     if bf and not _allow_variant:

@@ -158,6 +158,14 @@ class Validator:
         return True
 
 
+def slow_reversible_propose(partition):
+    """``grid_chain_sec11.py:117-130``: uniform over the (node, district) pairs of the pair
+    updater ``b_nodes`` (``:151-153``) registered under ``"b_nodes"`` (host use; the device
+    samples the same distribution, FC_PROPOSE_PAIR)."""
+    flip = random.choice(list(partition["b_nodes"]))
+    return partition.flip({flip[0]: flip[1]})
+
+
 def slow_reversible_propose_bi(partition):
     """``grid_chain_sec11.py:132-145`` (host use; the device samples the same distribution)."""
     fnode = random.choice(list(partition["b_nodes"]))
@@ -366,6 +374,10 @@ class ChainSpec:
     boundary_nodes: Optional[List[Hashable]] = None
     proposal: int = 0               # FC_PROPOSE_*
     recom: Optional[Dict[str, Any]] = None  # pop_target, epsilon, node_repeats
+    # slow_reversible_propose: |b_nodes| counts the pairs of the registered pair updater
+    # (FC_FLAG_NB_PAIRS), so geom_wait's p and the driver's rbn are what the reference computes
+    nb_pairs: bool = False
+    dev_labels: Optional[List[int]] = None  # int labels for the device's part_sum (None: indices)
 
 
 def _bounds_of(b) -> tuple:
@@ -377,14 +389,26 @@ def compile_chain(proposal, constraints, accept, initial_state: Partition) -> Ch
     """Map the reference's callables onto the device chain (NotImplementedError otherwise)."""
     import functools
     recom_kw = None
+    pair = False
     if isinstance(proposal, functools.partial) and getattr(proposal.func, "__name__", "") == "recom":
         kw = dict(proposal.keywords)
         recom_kw = {"pop_col": kw.get("pop_col", "population"), "pop_target": float(kw["pop_target"]),
                     "epsilon": float(kw["epsilon"]), "node_repeats": int(kw.get("node_repeats", 1))}
+    elif _name(proposal) == "slow_reversible_propose":
+        # grid_chain_sec11.py:117-130: random.choice(list(partition["b_nodes"])) over the pair
+        # updater b_nodes (:151-153) -> FC_PROPOSE_PAIR, any k
+        pair = True
+        bn = _name(initial_state.updaters.get("b_nodes"))
+        if "b_nodes" not in initial_state.updaters:
+            raise ValueError("slow_reversible_propose reads partition['b_nodes']: register the pair updater "
+                             "b_nodes (grid_chain_sec11.py:151-153)")
+        if bn != "b_nodes":
+            raise NotImplementedError(f"slow_reversible_propose with the 'b_nodes' updater {bn!r}: it draws "
+                                      "(node, district) pairs, so 'b_nodes' must be the pair updater b_nodes (:151-153)")
     elif _name(proposal) != "slow_reversible_propose_bi":
         raise NotImplementedError(f"proposal {_name(proposal)!r}: the device implements "
-                                  "slow_reversible_propose_bi (grid_chain_sec11.py:132-145) and "
-                                  "partial(recom, ...) (:328-335)")
+                                  "slow_reversible_propose_bi (grid_chain_sec11.py:132-145), "
+                                  "slow_reversible_propose (:117-130) and partial(recom, ...) (:328-335)")
     cons = constraints.constraints if isinstance(constraints, Validator) else (
         list(constraints) if isinstance(constraints, (list, tuple)) else [constraints])
     contig_idx, bounds, pop_key = None, None, "population"
@@ -440,13 +464,21 @@ def compile_chain(proposal, constraints, accept, initial_state: Partition) -> Ch
         raise NotImplementedError("the Validator's and the accept callable's population bounds differ")
     g = initial_state.graph
     labels = sorted(set(initial_state.assignment.values()))
+    if pair and len(labels) > 2:
+        if acc_kind != _lib.FC_ACCEPT_CUT or con_valid & ~(_lib.FC_CON_POP | _lib.FC_CON_CONTIG) or con_accept:
+            raise NotImplementedError("k > 2: the device runs the Validator([single_flip_contiguous, popbound]) + "
+                                      "cut_accept / always_accept chain (the accept / constraint variants are k = 2)")
+        if bounds is not None and contig_idx is not None and bounds[0] < contig_idx:
+            raise NotImplementedError("k > 2: the device's Validator tests single_flip_contiguous first")
+    if pair and len(labels) > 32:
+        raise NotImplementedError("the device holds at most 32 districts")
     if recom_kw is not None:
         if con_valid & ~(_lib.FC_CON_POP | _lib.FC_CON_CONTIG) or acc_kind != _lib.FC_ACCEPT_CUT:
             raise NotImplementedError("recom runs with the population Validator and cut_accept / always_accept")
         if recom_kw["pop_col"] != pop_key and bounds is not None:
             raise NotImplementedError("recom pop_col and the population bound must use the same column")
         pop_key = recom_kw["pop_col"]
-    elif len(labels) != 2 or sorted(labels) != [-1, 1]:
+    elif not pair and (len(labels) != 2 or sorted(labels) != [-1, 1]):
         raise NotImplementedError("slow_reversible_propose_bi flips -1 <-> 1: the plan must use labels -1 / 1")
     for n in g.nodes:
         g.nodes[n].setdefault(pop_key, 1)
@@ -466,12 +498,16 @@ def compile_chain(proposal, constraints, accept, initial_state: Partition) -> Ch
         if "boundary" not in initial_state.updaters:
             raise ValueError("boundary_condition reads partition['boundary']: add the 'boundary' updater")
         bnodes = list(initial_state["boundary"])
+    ints = all(isinstance(x, (int, np.integer)) and not isinstance(x, bool) and -2 ** 31 <= int(x) < 2 ** 31
+               for x in labels)
     return ChainSpec(spec=spec, labels=labels, init=init, base=base, pop_lo=lo, pop_hi=hi,
                      pop_bounds_float=(lo_f, hi_f), contig_first=contig_first, pop_key=pop_key,
                      accept=acc_kind, con_valid=con_valid, con_accept=con_accept, beta=beta, pinned=pinned,
                      frozen=frozen, boundary_nodes=bnodes,
-                     proposal=_lib.FC_PROPOSE_RECOM if recom_kw is not None else _lib.FC_PROPOSE_BI_SIGN,
-                     recom=recom_kw)
+                     proposal=_lib.FC_PROPOSE_RECOM if recom_kw is not None else
+                     _lib.FC_PROPOSE_PAIR if pair else _lib.FC_PROPOSE_BI_SIGN,
+                     recom=recom_kw, nb_pairs=pair and len(labels) > 2,
+                     dev_labels=[int(x) for x in labels] if ints else None)
 
 
 def check_device_constraints(cs: ChainSpec, graph) -> None:
@@ -594,12 +630,17 @@ class MarkovChain:
                             trace_cap=self.chunk + 16 if trace else 0, recom_pop_target=cs.recom["pop_target"],
                             recom_epsilon=cs.recom["epsilon"], recom_node_repeats=cs.recom["node_repeats"])
             return FlipRun(self._graph, cs.init[None, :], cfg)
-        cfg = RunConfig(seed=self.seed, chain_id_offset=self.chain_id, pop_lo=self.cspec.pop_lo,
-                        pop_hi=self.cspec.pop_hi, base=self.cspec.base, device=self.device, diag_mask=diag,
+        k = len(cs.labels)
+        # k > 2: the reference's Validator([single_flip_contiguous, popbound]) (or without a bound:
+        # the same with bounds nothing fails) is the kernels' default constraint set
+        con_valid = 0 if k > 2 else cs.con_valid
+        cfg = RunConfig(k=k, proposal=cs.proposal, seed=self.seed, chain_id_offset=self.chain_id,
+                        pop_lo=cs.pop_lo, pop_hi=cs.pop_hi, base=cs.base, device=self.device, diag_mask=diag,
+                        flags=_lib.FC_FLAG_NB_PAIRS if cs.nb_pairs else 0,
                         trace_chains=1 if trace else 0, trace_cap=64 * self.chunk + 4096 if trace else 0,
-                        labels=tuple(self.cspec.labels), event_cap=event_cap, accept=self.cspec.accept,
-                        con_valid=self.cspec.con_valid, con_accept=self.cspec.con_accept, beta=self.cspec.beta,
-                        frozen=tuple(self.cspec.frozen))
+                        labels=tuple(cs.dev_labels if cs.dev_labels is not None else range(k)),
+                        event_cap=event_cap, accept=cs.accept, con_valid=con_valid, con_accept=cs.con_accept,
+                        beta=cs.beta, frozen=tuple(cs.frozen))
         return FlipRun(self._graph, self.cspec.init[None, :], cfg)
 
     # ---- per-step iteration (debugging path) -------------------------------------------
@@ -624,7 +665,7 @@ class MarkovChain:
                 done += 1
                 if r["flags"] & 2:
                     v = int(r["v"])
-                    a[v] = 1 - a[v]
+                    a[v] = (int(r["flags"]) >> 8) & 0xff  # the target district (k = 2: 1 - a[v])
                     view = StateView(self, a.copy(), {sp.nodes[v]: lab[a[v]]}, int(r["wait"]), int(r["cut"]),
                                      int(r["nb"]), done - 1)
                 yield view
@@ -685,7 +726,9 @@ class MarkovChain:
         diag = _lib.FC_DIAG_WAIT | _lib.FC_DIAG_HIST | _lib.FC_DIAG_EDGES | _lib.FC_DIAG_FLIPS
         if frame == "auto":
             frame = None
-            if series and _name(self.initial_state.updaters.get("slope")) == "boundary_slope":
+            # (the frame-edge slope / angle of :371-394 is a two-district statistic; k = 2 only)
+            if series and len(self.cspec.labels) == 2 and \
+                    _name(self.initial_state.updaters.get("slope")) == "boundary_slope":
                 neg = any(isinstance(nd, tuple) and nd[1] < 0 for nd in self.cspec.spec.nodes)
                 frame = "frank" if neg else "sec11"
         if series:

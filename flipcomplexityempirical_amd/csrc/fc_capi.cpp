@@ -24,6 +24,8 @@ struct fc_run {
     fc_params p{};
     std::vector<int32_t> labels;
     std::vector<double> log1mp;
+    int32_t nb_w = 0;   // entries of the |B| histogram / log(1 - p) table: n + 1, or with
+                        // FC_FLAG_NB_PAIRS (k > 2) the largest pair count + 1
     int32_t n_chains = 0;
     int32_t npad = 0;
     int32_t words = 0;
@@ -227,6 +229,12 @@ int fc_device_count(int32_t *n) {
     return FC_OK;
 }
 
+int fc_device_pci_id(int32_t device, char *buf, int32_t cap) {
+    if (!buf || cap < 13) return fail(FC_ERR_ARG, "fc_device_pci_id: null buffer or cap < 13");
+    HIP_TRY(hipDeviceGetPCIBusId(buf, cap, device));
+    return FC_OK;
+}
+
 int fc_graph_create(int32_t n, const int32_t *row_ptr, const int32_t *col_idx, const int32_t *pop,
                     const double *pos_xy, uint32_t flags, fc_graph **out) {
     if (!out) return fail(FC_ERR_ARG, "fc_graph_create: null output");
@@ -296,6 +304,8 @@ int fc_params_init(fc_params *p, uint32_t struct_size) {
 int32_t fc_run_n_chains(const fc_run *r) { return r ? r->n_chains : 0; }
 
 int32_t fc_run_chain_lds_bytes(const fc_run *r) { return r ? r->chain_lds_bytes : 0; }
+
+int32_t fc_run_nb_width(const fc_run *r) { return r ? r->nb_w : 0; }
 
 int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, const int8_t *init_assign,
                   const double *bases, fc_run **out) {
@@ -371,12 +381,28 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     r->labels.resize(k);
     for (int i = 0; i < k; ++i) r->labels[i] = p->labels ? p->labels[i] : i;
     r->p.labels = nullptr;
-    r->log1mp.resize(n + 1);
+    // |b_nodes| as the driver's len(partition["b_nodes"]) counts it: nodes (b_nodes_bi, :155-156),
+    // or with FC_FLAG_NB_PAIRS the (node, district) pairs of the pair updater b_nodes (:151-153)
+    // a k > 2 driver registers for slow_reversible_propose (:117-130) -- at most
+    // sum_u min(deg u, k - 1).  With k = 2 both counts are the same.
+    const bool nb_pairs = (p->flags & FC_FLAG_NB_PAIRS) && k > 2;
+    if ((p->flags & FC_FLAG_NB_PAIRS) && recom)
+        return fail(FC_ERR_UNSUPPORTED, "fc_run_create: FC_FLAG_NB_PAIRS is for flip proposals");
+    r->nb_w = n + 1;
+    if (nb_pairs) {
+        int64_t mx = 0;
+        for (int32_t u = 0; u < n; ++u) mx += std::min<int64_t>(g.row_ptr[u + 1] - g.row_ptr[u], k - 1);
+        if (mx > 65535)  // fc_event.nb is 16 bits
+            return fail(FC_ERR_UNSUPPORTED, "fc_run_create: FC_FLAG_NB_PAIRS: more than 65535 possible pairs");
+        r->nb_w = (int32_t)mx + 1;
+    }
+    const int32_t nbw = r->nb_w;
+    r->log1mp.resize(nbw);
     if (p->log1mp) {
-        std::copy(p->log1mp, p->log1mp + n + 1, r->log1mp.begin());
+        std::copy(p->log1mp, p->log1mp + nbw, r->log1mp.begin());
     } else {
         const double denom = std::pow((double)n, (double)k) - 1.0;
-        for (int32_t b = 0; b <= n; ++b) r->log1mp[b] = std::log(1.0 - (double)b / denom);
+        for (int32_t b = 0; b < nbw; ++b) r->log1mp[b] = std::log(1.0 - (double)b / denom);
     }
     r->p.log1mp = nullptr;
     r->p.frozen = nullptr;
@@ -502,7 +528,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         if (t.deal != 1 && t.deal != -1) return fail(FC_ERR_ARG, "fc_run_create: tune_deal must be 1 or -1");
         t.deal = t.deal > 0 && k == 2 && !recom;
         const bool th_default = p->tune_prio_th[0] == 0.0f && p->tune_prio_th[1] == 0.0f && p->tune_prio_th[2] == 0.0f;
-        const float th0[3] = {0.95f, 1.0f, 1.05f};  // tools/gpu_knobs_r04.sh: 55.3 against 55.8 ms at {0.9, 1.0, 1.1}
+        const float th0[3] = {0.95f, 1.0f, 1.05f};  // tools/archive/gpu_knobs_r04.sh: 55.3 against 55.8 ms at {0.9, 1.0, 1.1}
         for (int i = 0; i < 3; ++i) t.prio_th[i] = th_default ? th0[i] : p->tune_prio_th[i];
     }
 
@@ -521,7 +547,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     const bool want_hist = p->diag_mask & FC_DIAG_HIST, want_edges = p->diag_mask & FC_DIAG_EDGES,
                want_flips = p->diag_mask & FC_DIAG_FLIPS;
     std::vector<int64_t> cut_hist, nb_hist, part_sum;
-    if (want_hist) { cut_hist.assign((size_t)n_chains * (E + 1), 0); nb_hist.assign((size_t)n_chains * (n + 1), 0); }
+    if (want_hist) { cut_hist.assign((size_t)n_chains * (E + 1), 0); nb_hist.assign((size_t)n_chains * nbw, 0); }
     if (want_flips) part_sum.assign((size_t)n_chains * n, 0);
     for (int32_t c = 0; c < n_chains; ++c) {
         const int8_t *a = init_assign + (size_t)c * n;
@@ -560,7 +586,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
                 nfh[(size_t)c * fc::kNfh + f] += 1;
             }
             fcnt[(size_t)c * r->npad + u] = (uint8_t)f;
-            nb += f > 0;
+            nb += nb_pairs ? f : f > 0;
         }
         if (band) {  // the band S of the initial state: b_nodes and their neighbours
             uint64_t *sb = &sbits[(size_t)c * r->words];
@@ -615,7 +641,7 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         s.sum_wait = wait0;
         if (want_hist) {
             cut_hist[(size_t)c * (E + 1) + cut] = 1;
-            nb_hist[(size_t)c * (n + 1) + nb] = 1;
+            nb_hist[(size_t)c * nbw + nb] = 1;
         }
         if (want_flips)
             for (int32_t u = 0; u < n; ++u) part_sum[(size_t)c * n + u] = r->labels[a[u]];  // :219
@@ -845,6 +871,8 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     k.flags = r->p.flags;
     k.cut_hist = r->d_cut_hist;
     k.nb_hist = r->d_nb_hist;
+    k.nb_w = r->nb_w;
+    k.nb_pairs = (r->p.flags & FC_FLAG_NB_PAIRS) && r->p.k > 2;
     k.edge_acc = r->d_edge_acc;
     k.num_flips = r->d_num_flips;
     k.part_sum = r->d_part_sum;
@@ -1115,7 +1143,7 @@ static std::vector<std::pair<void *, size_t>> ckpt_sections(fc_run *r) {
         }
     }
     if (r->d_cut_hist) v.emplace_back(r->d_cut_hist, C * (E + 1) * 8);
-    if (r->d_nb_hist) v.emplace_back(r->d_nb_hist, C * (n + 1) * 8);
+    if (r->d_nb_hist) v.emplace_back(r->d_nb_hist, C * (size_t)r->nb_w * 8);
     if (r->d_edge_acc) v.emplace_back(r->d_edge_acc, C * E * 8);
     if (r->d_num_flips) {
         v.emplace_back(r->d_num_flips, C * n * 8);
@@ -1717,7 +1745,7 @@ int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist) {
     if (!r->d_cut_hist) return fail(FC_ERR_ARG, "fc_run_read_hist: FC_DIAG_HIST not enabled");
     if (int rc = fc_run_sync(r)) return rc;
     HIP_TRY(hipMemcpy(cut_hist, r->d_cut_hist, (size_t)r->n_chains * (r->g.n_edges + 1) * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(nb_hist, r->d_nb_hist, (size_t)r->n_chains * (r->g.n + 1) * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(nb_hist, r->d_nb_hist, (size_t)r->n_chains * r->nb_w * 8, hipMemcpyDeviceToHost));
     return FC_OK;
 }
 
@@ -1796,15 +1824,15 @@ int fc_run_read_wait_expected(fc_run *r, double *out) {
     if (!r || !out) return fail(FC_ERR_ARG, "fc_run_read_wait_expected: null argument");
     if (!r->d_nb_hist) return fail(FC_ERR_ARG, "fc_run_read_wait_expected: FC_DIAG_HIST not enabled");
     if (int rc = fc_run_sync(r)) return rc;
-    const size_t n = r->g.n, C = r->n_chains;
-    std::vector<int64_t> h(C * (n + 1));
+    const size_t n = r->g.n, C = r->n_chains, W = (size_t)r->nb_w;
+    std::vector<int64_t> h(C * W);
     HIP_TRY(hipMemcpy(h.data(), r->d_nb_hist, h.size() * 8, hipMemcpyDeviceToHost));
     // geom_wait (:147-148): np.random.geometric(p) - 1 with p = |B| / (N^k - 1): mean 1/p - 1
     const double M = std::pow((double)n, (double)r->p.k) - 1.0;
     for (size_t c = 0; c < C; ++c) {
         double s = 0.0;
-        for (size_t b = 1; b <= n; ++b)
-            if (h[c * (n + 1) + b]) s += (double)h[c * (n + 1) + b] * (M / (double)b - 1.0);
+        for (size_t b = 1; b < W; ++b)
+            if (h[c * W + b]) s += (double)h[c * W + b] * (M / (double)b - 1.0);
         out[c] = s;
     }
     return FC_OK;

@@ -12,7 +12,7 @@
 // the schedule: a chain's trajectory depends on its own state and stream alone.
 //
 // C2 (ten bases dealt c % 10) does not need it: the dispatcher's order already gives every
-// SIMD one or two of the 1638 chains of bases 2.6-10 (tools/deal_prof.sh), and dealing by
+// SIMD one or two of the 1638 chains of bases 2.6-10 (tools/archive/deal_prof.sh), and dealing by
 // draws measured 72.8-75.1 ms per launch against 74.4-74.5 without, so it is off by default
 // (fc_params.tune_deal = 1 turns it on).
 #include <hip/hip_runtime.h>

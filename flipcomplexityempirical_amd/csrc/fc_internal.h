@@ -99,13 +99,15 @@ struct KParams {
     uint8_t *fcnt;              // [n_chains * n] foreign-neighbour counts
     ChainScalars *sc;           // [n_chains]
     const uint64_t *thresh;     // [n_chains * (2*RMAX+1)] acceptance thresholds (U53 mantissa)
-    const double *log1mp;       // [n + 1]
+    const double *log1mp;       // [nb_w]
     const int32_t *labels;      // [k]
     uint32_t diag;              // FC_DIAG_*
     uint32_t flags;             // FC_FLAG_*
     // optional diagnostics
     int64_t *cut_hist;          // [n_chains * (E+1)]
-    int64_t *nb_hist;           // [n_chains * (n+1)]
+    int64_t *nb_hist;           // [n_chains * nb_w]
+    int32_t nb_w;               // |B| histogram row: n + 1, or the largest pair count + 1 (nb_pairs)
+    int32_t nb_pairs;           // k > 2, FC_FLAG_NB_PAIRS: |B| counts (node, district) pairs
     int64_t *edge_acc;          // [n_chains * E]
     int64_t *num_flips;         // [n_chains * n]
     int64_t *part_sum;          // [n_chains * n]

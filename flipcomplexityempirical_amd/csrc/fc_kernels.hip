@@ -860,6 +860,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                         if (app && nb_m && nfn_m != old_m) pkb[um] = (uint8_t)(au_m | ((nfn_m < 7 ? nfn_m : 7) << 5));
                         const bool ent_m = app && nb_m && old_m == 0 && nfn_m > 0;
                         const bool lev_m = app && nb_m && old_m > 0 && nfn_m == 0;
+                        // FC_FLAG_NB_PAIRS: |B| counts (node, district) pairs -- each flip's change
+                        // is its neighbours' nf changes plus its own node's, summed over lane groups
+                        int pscan = 0;
+                        if (p.nb_pairs)
+                            pscan = wave_scan_incl((app && nb_m ? nfn_m - old_m : 0) +
+                                                   (app && ge == 0 ? nf_af - nf_bf : 0));
                         // the slots up to the last flip applied: verdict bits, |cut| / |B| after each flip
                         const int fl = nA_ == nF ? f_last : select_bit64(FM, nA_ - 1);
                         if (prop && lane >= f && lane <= fl) st |= bits;
@@ -876,14 +882,15 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                                 my_cs = rk == g ? csum : my_cs;
                             }
                         const uint64_t ENT = __ballot(ent_m), LEV = __ballot(lev_m);
+                        const int pupto = p.nb_pairs ? __shfl(pscan, ((rk + 1) * RMAX - 1) & 63) : 0;
                         if (((FM >> lane) & 1ull) && rk < nA_) {
                             const uint64_t upto = bits_below((rk + 1) * RMAX);
                             st |= ST_VS | ST_AC;
                             cut_after = cut + my_cs;
-                            nb_after = nb + __popcll(ENT & upto) - __popcll(LEV & upto);
+                            nb_after = p.nb_pairs ? nb + pupto : nb + __popcll(ENT & upto) - __popcll(LEV & upto);
                         }
                         cut += csum;
-                        nb += __popcll(ENT) - __popcll(LEV);
+                        nb += p.nb_pairs ? rl32(pscan, 63) : __popcll(ENT) - __popcll(LEV);
                         rem -= __popcll(VAL & lane_range(f, fl + 1));
                         last_flip = rl32(v, fl);
                         compiler_fence();
@@ -927,6 +934,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
             FC_STAMP(t_g1);
             bool enter = false, leave = false, grew = false;
             bool wcap_chg = false;
+            int dpair = 0;  // FC_FLAG_NB_PAIRS: this lane's change of the (node, district) pair count
             if constexpr (KM == 2) {
                 // foreign-neighbour counts: u sees v leave A (+1 if u in A) and join t (-1 if u in t)
                 const int dlt = (int)((inAf >> lane) & 1u) - (int)((tmf >> lane) & 1u);
@@ -981,10 +989,12 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                     enter = old == 0 && nfn > 0;
                     leave = old > 0 && nfn == 0;
                     grew = nfn > old;
+                    dpair = nfn - old;
                 }
                 if (lane == 0) {
                     // vf's own count: before / after from its evaluation (its view was current)
                     const int old = PK ? nf_bf : (int)fcnt[vf];
+                    dpair += nf_af - old;
                     if (nf_af != old) {
                         if constexpr (!PK) fcnt[vf] = (uint8_t)nf_af;
                         atomicSub(&nfh[old], 1);
@@ -1007,7 +1017,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
             // non-hit draws to re-check below: nodes that entered the boundary; with PAIR
             // slots any node whose foreign-district count grew (its slot may now fall below it)
             uint64_t ent = __ballot(grew);
-            const int dnb = __popcll(__ballot(enter)) - __popcll(__ballot(leave));
+            int dnb = __popcll(__ballot(enter)) - __popcll(__ballot(leave));
+            if constexpr (KM != 2)
+                if (p.nb_pairs) dnb = rl32(wave_scan_incl(dpair), 63);
             // district-graph tables: the pairs {vf, w} of vf's face-adjacent cells w move from
             // (Af, a[w]) to (tf, a[w]); a count crossing 0 flips an adjacency bit (as does an
             // outer-face node crossing between districts), which may change the verdict of a
@@ -1212,11 +1224,11 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
             if (p.diag & FC_DIAG_HIST) {
                 if (is_acc) {
                     atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut_after], (unsigned long long)run_len);
-                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb_after], (unsigned long long)run_len);
+                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * p.nb_w + nb_after], (unsigned long long)run_len);
                 }
                 if (lane == 0 && r0) {
                     atomicAdd((unsigned long long *)&p.cut_hist[(size_t)c * (p.n_edges + 1) + cut0], (unsigned long long)r0);
-                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * (n + 1) + nb0], (unsigned long long)r0);
+                    atomicAdd((unsigned long long *)&p.nb_hist[(size_t)c * p.nb_w + nb0], (unsigned long long)r0);
                 }
             }
             if (p.diag & FC_DIAG_FLIPS) {

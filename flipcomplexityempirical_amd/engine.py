@@ -15,7 +15,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check
-from .graphs import GraphSpec, log1mp_table
+from .graphs import GraphSpec, log1mp_table, nb_width
 
 _P = ctypes.POINTER
 
@@ -184,8 +184,12 @@ class FlipRun:
             raise ValueError("init_assign must have one entry per node")
         labels = list(cfg.labels) if len(cfg.labels) == cfg.k else list(range(cfg.k))
         self._labels = np.ascontiguousarray(labels, dtype=np.int32)
-        self._log1mp = np.ascontiguousarray(log1mp if log1mp is not None else log1mp_table(graph.n, cfg.k),
+        pairs = bool(cfg.flags & _lib.FC_FLAG_NB_PAIRS) and cfg.k > 2
+        width = nb_width(graph.spec, cfg.k, True) if pairs else graph.n + 1
+        self._log1mp = np.ascontiguousarray(log1mp if log1mp is not None else log1mp_table(graph.n, cfg.k, width),
                                             dtype=np.float64)
+        if self._log1mp.size < width:
+            raise ValueError(f"log1mp needs {width} entries (|b_nodes| 0 .. {width - 1})")
         self._bases = None if bases is None else np.ascontiguousarray(bases, dtype=np.float64)
         if self._bases is not None and self._bases.shape[0] != self.n_chains:
             raise ValueError("bases must have one entry per chain")
@@ -327,7 +331,7 @@ class FlipRun:
     def hist(self):
         E, n = self.graph.n_edges, self.graph.n
         ch = np.zeros((self.n_chains, E + 1), dtype=np.int64)
-        nh = np.zeros((self.n_chains, n + 1), dtype=np.int64)
+        nh = np.zeros((self.n_chains, self.nb_width()), dtype=np.int64)
         check(_lib.load().fc_run_read_hist(self.handle, _p(ch, ctypes.c_int64), _p(nh, ctypes.c_int64)))
         return ch, nh
 
@@ -530,6 +534,11 @@ class FlipRun:
         ev = self.events(chain)
         bounds = np.concatenate([[t0], ev["t"], [T + 1]]).astype(np.int64)
         return np.repeat(np.asarray(values)[:ev.size + 1], np.diff(bounds))
+
+    def nb_width(self) -> int:
+        """Entries of a chain's |B| histogram row (``fc_run_nb_width``): n + 1, or the largest
+        pair count + 1 with ``FC_FLAG_NB_PAIRS``."""
+        return int(_lib.load().fc_run_nb_width(self.handle))
 
     def chain_lds_bytes(self) -> int:
         """LDS bytes of one chain's device state (``fc_run_chain_lds_bytes``)."""

@@ -400,9 +400,21 @@ def population_bounds(total_pop: int, k: int, percent: float):
     return (lo, hi), (int(math.ceil(lo)), int(math.floor(hi)))
 
 
-def log1mp_table(n_nodes: int, k: int) -> np.ndarray:
-    """``log(1 - p)`` for ``p = |B| / (N**k - 1)``, |B| = 0..N -- the exact float pipeline of
-    ``geom_wait`` (``grid_chain_sec11.py:147-148``: Python true division of ints, then numpy's
-    legacy ``log(1.0 - p)``)."""
+def log1mp_table(n_nodes: int, k: int, width: Optional[int] = None) -> np.ndarray:
+    """``log(1 - p)`` for ``p = |B| / (N**k - 1)``, |B| = 0..N (or 0..width-1: |b_nodes| counted
+    as pairs, ``nb_width``) -- the exact float pipeline of ``geom_wait``
+    (``grid_chain_sec11.py:147-148``: Python true division of ints, then numpy's legacy
+    ``log(1.0 - p)``)."""
     denom = n_nodes ** k - 1
-    return np.asarray([math.log(1.0 - (b / denom)) for b in range(n_nodes + 1)], dtype=np.float64)
+    return np.asarray([math.log(1.0 - (b / denom)) for b in range(width or n_nodes + 1)], dtype=np.float64)
+
+
+def nb_width(spec: "GraphSpec", k: int, pairs: bool) -> int:
+    """Entries of a |B| histogram row / log(1 - p) table (``fc_run_nb_width``): n + 1, or, with
+    |b_nodes| counted as the (node, district) pairs of the pair updater ``b_nodes``
+    (``grid_chain_sec11.py:151-153``; ``FC_FLAG_NB_PAIRS``, k > 2), the largest pair count
+    sum_u min(deg u, k - 1), plus one."""
+    if not pairs or k <= 2:
+        return spec.n + 1
+    deg = np.diff(np.asarray(spec.row_ptr, dtype=np.int64))
+    return int(np.minimum(deg, k - 1).sum()) + 1

@@ -92,6 +92,13 @@ extern "C" {
                                     chains fill it and apply the rest of a launch's tallies with
                                     atomics -- the path a device short of memory takes; same
                                     output (a cross-check)                                      */
+#define FC_FLAG_NB_PAIRS 0x8u    /* k > 2 PAIR runs: |b_nodes| (stats nb / sum_nb, the |B| histogram,
+                                    geom_wait's p = |b_nodes| / (N^k - 1)) counts the (node,
+                                    district) pairs of the pair updater b_nodes (:151-153), which a
+                                    k > 2 driver running slow_reversible_propose (:117-130)
+                                    registers as "b_nodes", instead of the nodes of b_nodes_bi
+                                    (:155-156).  The histogram and log1mp then have
+                                    fc_run_nb_width entries; no-op for k = 2                     */
 
 typedef struct fc_graph fc_graph;
 typedef struct fc_run fc_run;
@@ -124,7 +131,8 @@ typedef struct fc_params {
     int32_t trace_chains;      /* chains 0..trace_chains-1 record per-proposal traces      */
     int64_t trace_cap;         /* records per traced chain                                  */
     const int32_t *labels;     /* [k] reference district labels (e.g. -1, 1); NULL = 0..k-1 */
-    const double *log1mp;      /* [n+1] log(1 - b/(N^k - 1)); NULL = computed in double     */
+    const double *log1mp;      /* [n+1] log(1 - b/(N^k - 1)) ([fc_run_nb_width] with
+                                  FC_FLAG_NB_PAIRS); NULL = computed in double               */
     int32_t wmax;              /* PAIR: district slots per node draw (<= 0: min(max deg, k-1)) */
     int32_t hit_lo, hit_hi;    /* hitting time: first yield with hit_lo <= |cut| <= hit_hi
                                   (hit_lo > hit_hi: off)                                     */
@@ -314,7 +322,7 @@ int fc_run_read_trace(fc_run *r, int32_t chain, fc_record *out, int64_t cap, int
 int fc_run_read_recom_trace(fc_run *r, int32_t chain, fc_recom_record *out, int64_t cap, int64_t *len);
 /* Restart every traced chain's record buffer at 0 (chunked per-step iteration). */
 int fc_run_trace_reset(fc_run *r);
-int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist);      /* [c*(E+1)], [c*(n+1)] */
+int fc_run_read_hist(fc_run *r, int64_t *cut_hist, int64_t *nb_hist);      /* [c*(E+1)], [c*nb_width] */
 int fc_run_read_edges(fc_run *r, int64_t *cut_times);                     /* [c*E], finalised     */
 /* num_flips / part_sum / last_flipped [c*n], finalised as grid_chain_sec11.py:416-418. */
 int fc_run_read_flips(fc_run *r, int64_t *num_flips, int64_t *part_sum, int64_t *last_flipped);
@@ -397,9 +405,15 @@ int32_t fc_run_n_chains(const fc_run *r);
  * holds at once is 160 KiB / this, or the VGPR limit) -- for sizing launches to one wave of
  * resident chains. */
 int32_t fc_run_chain_lds_bytes(const fc_run *r);
+/* Entries of a chain's |B| histogram row and of the log1mp table: n + 1, or with
+ * FC_FLAG_NB_PAIRS (k > 2) sum_u min(deg u, k - 1) + 1, the largest pair count + 1. */
+int32_t fc_run_nb_width(const fc_run *r);
 void fc_run_destroy(fc_run *r);
 
 int fc_device_count(int32_t *n);
+/* PCI bus id ("dddd:bb:dd.f") of HIP device `device` (hipDeviceGetPCIBusId): an N-GPU bench line
+ * lists every rank's, so it shows that N distinct GPUs did the work. */
+int fc_device_pci_id(int32_t device, char *buf, int32_t cap);
 const char *fc_last_error(void);
 
 /* What this library was built with (FC_BUILD_* bits; 0 = the product build).  A profiling or

@@ -69,6 +69,12 @@ static int in_boundary(const ctx_t *c, int32_t u) {
     return 0;
 }
 
+/* u's share of |b_nodes|: 1 if u is a boundary node (b_nodes_bi, :155-156), or with
+ * nb_pairs its number of (u, district) pairs in b_nodes (:151-153) */
+static int32_t nb_of(const ctx_t *c, int32_t u) {
+    return c->p->nb_pairs ? n_foreign(c, u) : in_boundary(c, u);
+}
+
 /* single_flip_contiguous [gc-0.2] restated: old_nbrs = neighbours still in v's old
  * district; empty => invalid; else every old neighbour must reach one fixed old neighbour
  * through the old district with v removed (the canonical stream omits the random.choice
@@ -243,12 +249,12 @@ static int fixed_ok_after(const ctx_t *c, int32_t v, int8_t T) {
  * partition and partition.parent in annealing_cut_accept_backwards, :82-83). */
 static int32_t nb_after_flip(ctx_t *c, int32_t v, int8_t T) {
     const fr_params *p = c->p;
-    int32_t before = in_boundary(c, v), after;
-    for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) before += in_boundary(c, p->col_idx[j]);
+    int32_t before = nb_of(c, v), after;
+    for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) before += nb_of(c, p->col_idx[j]);
     const int8_t A = c->a[v];
     c->a[v] = T;
-    after = in_boundary(c, v);
-    for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) after += in_boundary(c, p->col_idx[j]);
+    after = nb_of(c, v);
+    for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) after += nb_of(c, p->col_idx[j]);
     c->a[v] = A;
     return c->nb + after - before;
 }
@@ -320,11 +326,19 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
     if ((con_valid & FR_CON_FIXED) && !fixed_ok_after(&c, 0, c.a[0])) { rc = -1; goto done; }
 
     for (int32_t e = 0; e < c.n_edges; ++e) c.cut += c.a[c.eu[e]] != c.a[c.ev[e]];
-    for (int32_t u = 0; u < n; ++u) c.nb += in_boundary(&c, u);
+    int32_t nb_max = n;
+    if (p->nb_pairs) {
+        nb_max = 0;
+        for (int32_t u = 0; u < n; ++u) {
+            const int32_t dg = p->row_ptr[u + 1] - p->row_ptr[u];
+            nb_max += dg < p->k - 1 ? dg : p->k - 1;
+        }
+    }
+    for (int32_t u = 0; u < n; ++u) c.nb += nb_of(&c, u);
     if (o) {
         if (o->cut_times) memset(o->cut_times, 0, sizeof(int64_t) * (size_t)c.n_edges);
         if (o->cut_hist) memset(o->cut_hist, 0, sizeof(int64_t) * (size_t)(c.n_edges + 1));
-        if (o->nb_hist) memset(o->nb_hist, 0, sizeof(int64_t) * (size_t)(n + 1));
+        if (o->nb_hist) memset(o->nb_hist, 0, sizeof(int64_t) * (size_t)(nb_max + 1));
         if (o->num_flips)
             for (int32_t u = 0; u < n; ++u) {
                 o->num_flips[u] = 0; o->last_flipped[u] = 0;
@@ -454,14 +468,14 @@ int fr_run(const fr_params *p, const int8_t *init_assign, fr_stats *st, fr_outpu
         const double U = u53(w[1], w[2]);
         const int acc = U < bound;
         if (acc) {
-            int32_t before = in_boundary(&c, v), after;
-            for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) before += in_boundary(&c, p->col_idx[j]);
+            int32_t before = nb_of(&c, v), after;
+            for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) before += nb_of(&c, p->col_idx[j]);
             c.a[v] = T;
             c.pops[A] -= p->pop[v];
             c.pops[T] += p->pop[v];
             c.cut += delta;
-            after = in_boundary(&c, v);
-            for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) after += in_boundary(&c, p->col_idx[j]);
+            after = nb_of(&c, v);
+            for (int32_t j = p->row_ptr[v]; j < p->row_ptr[v + 1]; ++j) after += nb_of(&c, p->col_idx[j]);
             c.nb += after - before;
             st->accepted += 1;
             st->last_flip = v;

@@ -102,6 +102,12 @@ typedef struct fr_params {
      * plus their neighbours, recomputed after an accepted flip only when a node enters b_nodes
      * outside S.  Either is rejection sampling of random.choice(b_nodes)   */
     int32_t stream;
+    /* |b_nodes| counted as the (node, district) pairs of the pair updater b_nodes
+     * (grid_chain_sec11.py:151-153) instead of the nodes of b_nodes_bi (:155-156): what
+     * len(partition["b_nodes"]) is in a k > 2 driver that runs slow_reversible_propose (:117-130),
+     * in stats.nb, sum_nb, the |B| histogram ([nb_max + 1], nb_max = sum_u min(deg u, k - 1)) and
+     * geom_wait's p (:147-148, log1mp then [nb_max + 1]).  With k = 2 both counts coincide. */
+    int32_t nb_pairs;
 } fr_params;
 
 #define FR_STREAM_NODE 0
@@ -123,7 +129,8 @@ typedef struct fr_outputs {
     fr_record *trace; int64_t trace_cap; int64_t trace_len;   /* nullable trace      */
     int8_t *final_assign;                                     /* [n]                 */
     int64_t *cut_hist;                                        /* [E+1] nullable      */
-    int64_t *nb_hist;                                         /* [n+1] nullable      */
+    int64_t *nb_hist;                                         /* [n+1] nullable ([nb_max+1]
+                                                                 with nb_pairs)      */
     int64_t *cut_times;                                       /* [E]   nullable      */
     int64_t *num_flips, *part_sum, *last_flipped;             /* [n]   nullable      */
     /* corrected companions, [n] nullable together:

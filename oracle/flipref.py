@@ -125,7 +125,7 @@ class FrParams(ctypes.Structure):
                 ("accept", ctypes.c_int32), ("con_valid", ctypes.c_uint32), ("con_accept", ctypes.c_uint32),
                 ("beta", ctypes.c_double), ("boundary", _P(ctypes.c_uint8)), ("pinned", _P(ctypes.c_int32)),
                 ("n_pinned", ctypes.c_int32), ("wait0_words", _P(ctypes.c_uint32)),
-                ("stream", ctypes.c_int32)]
+                ("stream", ctypes.c_int32), ("nb_pairs", ctypes.c_int32)]
 
 
 ACCEPT_CUT, ACCEPT_UNIFORM, ACCEPT_ANNEAL = 0, 1, 2
@@ -171,6 +171,16 @@ def _ptr(arr, ctype):
     return arr.ctypes.data_as(ctypes.POINTER(ctype))
 
 
+def nb_width(spec, k: int, nb_pairs: bool) -> int:
+    """Entries of the |B| histogram / log(1 - p) table: n + 1, or with ``nb_pairs`` (|b_nodes|
+    counted as the pair updater's (node, district) pairs, grid_chain_sec11.py:151-153) one more
+    than the largest pair count, sum_u min(deg u, k - 1)."""
+    if not nb_pairs:
+        return spec.n + 1
+    deg = np.diff(np.asarray(spec.row_ptr, dtype=np.int64))
+    return int(np.minimum(deg, k - 1).sum()) + 1
+
+
 class CRef:
     """The plain-C oracle.  ``run`` restates one chain from its initial state."""
 
@@ -213,7 +223,7 @@ class CRef:
             accept: int = 0, con_valid: int = 0, con_accept: int = 0, beta: float = 0.0,
             boundary: Optional[np.ndarray] = None, pinned: Optional[np.ndarray] = None,
             wait0_words: Optional[np.ndarray] = None, want_exact_flips: bool = False,
-            stream: int = STREAM_NODE) -> Dict:
+            stream: int = STREAM_NODE, nb_pairs: bool = False) -> Dict:
         n, E = spec.n, spec.n_edges
         row_ptr = np.ascontiguousarray(spec.row_ptr, dtype=np.int32)
         col_idx = np.ascontiguousarray(spec.col_idx, dtype=np.int32)
@@ -236,11 +246,12 @@ class CRef:
                      proposal=int(proposal), wmax=int(wmax), accept=int(accept), con_valid=int(con_valid),
                      con_accept=int(con_accept), beta=float(beta), boundary=_ptr(bnd, ctypes.c_uint8),
                      pinned=_ptr(pin, ctypes.c_int32), n_pinned=0 if pin is None else pin.size // 2,
-                     wait0_words=_ptr(w0, ctypes.c_uint32), stream=int(stream))
+                     wait0_words=_ptr(w0, ctypes.c_uint32), stream=int(stream), nb_pairs=int(bool(nb_pairs)))
         trace = np.zeros(trace_cap, dtype=RECORD_DTYPE) if trace_cap else None
         final = np.zeros(n, dtype=np.int8)
         cut_hist = np.zeros(E + 1, dtype=np.int64) if want_hist else None
-        nb_hist = np.zeros(n + 1, dtype=np.int64) if want_hist else None
+        nb_w = nb_width(spec, k, nb_pairs)
+        nb_hist = np.zeros(nb_w, dtype=np.int64) if want_hist else None
         cut_times = np.zeros(E, dtype=np.int64) if want_edges else None
         nf = np.zeros(n, dtype=np.int64) if want_flips else None
         ps = np.zeros(n, dtype=np.int64) if want_flips else None
@@ -396,8 +407,12 @@ class GcFaithfulChain:
 
     def __init__(self, spec, plan: Dict, *, base: float, pop_bounds, seed: int, chain_id: int,
                  log1mp: Optional[np.ndarray] = None, tape: Optional[np.ndarray] = None,
-                 pair: bool = False, wmax: int = 0, band: bool = False):
+                 pair: bool = False, wmax: int = 0, band: bool = False, nb_pairs: bool = False):
         self.spec = spec
+        # |b_nodes| as len(partition["b_nodes"]) sees it: the nodes of b_nodes_bi (:155-156), or
+        # with nb_pairs the (node, district) pairs of the pair updater b_nodes (:151-153), which a
+        # k > 2 driver running slow_reversible_propose registers as "b_nodes"
+        self.nb_key = "pairs" if nb_pairs else "b_nodes"
         self.g = spec.nx_graph
         self.base = base
         self.lo, self.hi = pop_bounds  # float bounds, exactly as Bounds compares
@@ -451,7 +466,7 @@ class GcFaithfulChain:
             return 0
         w = self._words(d, purpose)
         U = u53(w[0], w[1])
-        nb = len(self.state["b_nodes"])
+        nb = len(self.state[self.nb_key])
         l1 = self.log1mp[nb]
         q = math.log(1.0 - U) / l1 if l1 != 0.0 else -math.inf
         if not abs(q) < 2.0 ** 62:
@@ -461,7 +476,7 @@ class GcFaithfulChain:
     def _yield(self):
         s = self.state
         self.stats["sum_cut"] += len(s["cut_edges"])
-        self.stats["sum_nb"] += len(s["b_nodes"])
+        self.stats["sum_nb"] += len(s[self.nb_key])
         self.stats["sum_wait"] += self.wait
 
     def _valid(self, proposal):
@@ -508,7 +523,7 @@ class GcFaithfulChain:
             bad = self._valid(proposal)
             if bad:
                 self.stats["inv_contig" if bad == FLAG_INV_CONTIG else "inv_pop"] += 1
-                self.trace.append((draw, self.spec.index[node], bad | tid, len(s["cut_edges"]), len(s["b_nodes"]), 0))
+                self.trace.append((draw, self.spec.index[node], bad | tid, len(s["cut_edges"]), len(s[self.nb_key]), 0))
                 continue
             self.stats["steps"] += 1
             bound = self.base ** (-len(proposal["cut_edges"]) + len(s["cut_edges"]))  # :175
@@ -522,7 +537,7 @@ class GcFaithfulChain:
             self._yield()
             cur = self.state
             self.trace.append((draw, self.spec.index[node], FLAG_VALID | (FLAG_ACCEPTED if acc else 0) | tid,
-                               len(cur["cut_edges"]), len(cur["b_nodes"]), self.wait))
+                               len(cur["cut_edges"]), len(cur[self.nb_key]), self.wait))
             return cur
 
     def run(self, n_steps: int):
@@ -555,13 +570,16 @@ class NativeRngChain(GcFaithfulChain):
     ``random.choice(list(pairs))`` over the (node, district) pairs of ``b_nodes`` (:151-153),
     then ``partition.flip({node: district})``.  The pair set is the proposal's own (the inline
     form commented at :125-126); the ``"b_nodes"`` updater stays ``b_nodes_bi`` as registered at
-    :305, so ``geom_wait`` (:148) and the driver's ``rbn`` (:369) keep counting nodes.  The node
+    :305, so ``geom_wait`` (:148) and the driver's ``rbn`` (:369) keep counting nodes; with
+    ``nb_pairs=True`` they count the pairs instead, as in a driver that registers the pair updater
+    ``b_nodes`` under ``"b_nodes"`` (which ``slow_reversible_propose`` reads, :128).  The node
     tape then also carries word 3: the Lemire word that sends the state's slot bound ``wcap``
     (its largest foreign-district count, the canonical PAIR stream's bound) to the drawn
     district's rank among the node's foreign districts, ascending."""
 
     def __init__(self, spec, plan: Dict, *, base: float, pop_bounds, seed: int,
-                 log1mp: Optional[np.ndarray] = None, record: bool = False, pair: bool = False):
+                 log1mp: Optional[np.ndarray] = None, record: bool = False, pair: bool = False,
+                 nb_pairs: bool = False):
         import random as _random
         self.rng = _random.Random(seed)
         self.nprng = np.random.RandomState(seed & 0xFFFFFFFF)
@@ -570,7 +588,7 @@ class NativeRngChain(GcFaithfulChain):
         self.wait0_words = None
         self._geom_words = None   # words of the last geometric draw
         super().__init__(spec, plan, base=base, pop_bounds=pop_bounds, seed=seed, chain_id=0, log1mp=log1mp,
-                         pair=pair)
+                         pair=pair, nb_pairs=nb_pairs)
         if record:
             self.wait0_words = self._geom_words
 
@@ -606,14 +624,14 @@ class NativeRngChain(GcFaithfulChain):
         if self.log1mp is None:
             return 0
         s = self.state
-        p = len(list(s["b_nodes"])) / (len(self.g.nodes) ** len(self.labels) - 1)  # :148
+        p = len(list(s[self.nb_key])) / (len(self.g.nodes) ** len(self.labels) - 1)  # :148
         if self.record:
             clone = np.random.RandomState()
             clone.set_state(self.nprng.get_state())
             U = clone.random_sample()
             self._geom_words = self._u53_words(U)
         w = int(self.nprng.geometric(p, 1)[0]) - 1
-        nb = len(s["b_nodes"])
+        nb = len(s[self.nb_key])
         if float(self.log1mp[nb]) == 0.0:
             # 1 - p rounds to 1.0 (N^k beyond 2^53 |B|, e.g. k = 8 on 3,120 nodes): numpy's
             # inversion divides by log(1.0) = 0 and casts +inf to int64, which gives INT64_MIN;
@@ -651,7 +669,7 @@ class NativeRngChain(GcFaithfulChain):
                 if self.record:
                     self.tape_words.extend(words)
                     self.trace.append((draw, self.spec.index[node], bad | tid, len(s["cut_edges"]),
-                                       len(s["b_nodes"]), 0))
+                                       len(s[self.nb_key]), 0))
                 continue
             self.stats["steps"] += 1
             bound = self.base ** (-len(proposal["cut_edges"]) + len(s["cut_edges"]))  # :175
@@ -672,7 +690,7 @@ class NativeRngChain(GcFaithfulChain):
                 self.tape_words.extend(words)
                 cur = self.state
                 self.trace.append((draw, self.spec.index[node], FLAG_VALID | (FLAG_ACCEPTED if acc else 0) | tid,
-                                   len(cur["cut_edges"]), len(cur["b_nodes"]), self.wait))
+                                   len(cur["cut_edges"]), len(cur[self.nb_key]), self.wait))
             return self.state
 
     def node_tape(self) -> np.ndarray:

@@ -33,7 +33,11 @@ def test_gpus_n_launches_n_ranks():
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
         assert len(lines) == 1, r.stdout  # rank 0 alone prints
         rec = json.loads(lines[0])
+        devs = rec.pop("devices")
         assert rec == {"ranks_seen": n, "rank_sum": float(n * (n - 1) // 2), "launcher": "bench.py"}
+        # every rank's device identity, and that they are distinct
+        assert [d["rank"] for d in devs["per_rank"]] == list(range(n)) and devs["distinct"] is True
+        assert [d["local_rank"] for d in devs["per_rank"]] == list(range(n))
 
 
 def test_failing_rank_fails_the_launch():

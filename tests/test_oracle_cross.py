@@ -66,22 +66,26 @@ def test_oracle_stuck_cap(cref, sec11):
     assert r["stats"]["inv_pop"] > 0
 
 
+@pytest.mark.parametrize("nb_pairs", [False, True])
 @pytest.mark.parametrize("which,k,base", [("sec11", 4, G.SEC11_MU), ("sec11", 4, 0.5), ("tri", 8, 1.0)])
-def test_c_oracle_pair_equals_gc_faithful(cref, sec11, which, k, base):
+def test_c_oracle_pair_equals_gc_faithful(cref, sec11, which, k, base, nb_pairs):
     """PAIR proposals (slow_reversible_propose over b_nodes pairs, grid_chain_sec11.py:117-130,
-    151-153) for k > 2: the C restatement equals the gerrychain-faithful one."""
+    151-153) for k > 2: the C restatement equals the gerrychain-faithful one -- with |b_nodes|
+    counted as nodes (b_nodes_bi) or, ``nb_pairs``, as the pair updater's pairs (what
+    len(part["b_nodes"]) is in a driver that registers it: rbn, and geom_wait's p)."""
     from oracle.flipref import GcFaithfulChain
     spec = sec11 if which == "sec11" else G.triangular_graph(12, 22)
     plan = G.quadrant_plan(spec.nodes) if which == "sec11" else G.strip_plan(spec, k)
     labels = list(range(k))
     a0 = spec.assignment_array(plan, labels)
-    l1 = G.log1mp_table(spec.n, k)
+    l1 = G.log1mp_table(spec.n, k, G.nb_width(spec, k, nb_pairs))
     pct = 0.05 if which == "sec11" else 0.1
     (lo, hi), (ilo, ihi) = G.population_bounds(int(spec.pop.sum()), k, pct)
     gc = GcFaithfulChain(spec, plan, base=base, pop_bounds=(lo, hi), seed=5, chain_id=2, log1mp=l1,
-                         pair=True).run(300)
+                         pair=True, nb_pairs=nb_pairs).run(300)
     r = cref.run(spec, a0, base=base, pop_lo=ilo, pop_hi=ihi, seed=5, chain_id=2, n_steps=300, k=k,
-                 labels=labels, log1mp=l1, trace_cap=100000, proposal=1)
+                 labels=labels, log1mp=l1, trace_cap=100000, proposal=1, nb_pairs=nb_pairs, want_hist=True)
+    assert r["nb_hist"].size == l1.size and r["nb_hist"].sum() == 301
     gtr = np.array(gc.trace, dtype=np.int64)
     tr = r["trace"]
     assert len(tr) == len(gtr) and len(tr) > 300

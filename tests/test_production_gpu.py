@@ -1,5 +1,11 @@
-"""The k > 2 kernels at production shape.
+"""The kernels the bench times, at production shape (VERDICT r05
+item 1).
 
+* C2 (the headline, BASELINE config 2): bench.py's own workload object -- 4096 chains, base
+  ``bases[g % 10]``, alignment ``(g // 10) % 3``, pop 0.1, seed 0x5EED0002 -- one 100,000-step
+  launch of the lean instance bench.py times, 48 chains sampled over the id range (every (base,
+  alignment) configuration of the two short-boundary bases 6.96 / 10 among them) against the C
+  oracle: final state and every counter (``grid_chain_sec11.py:340-342,366-411``).
 * C3 (BASELINE config 3: sec11 lattice, k = 4 quadrant plan, pair proposals, population
   tolerance 0.05, base mu, 8192 chains per GPU, the multi-flip commit on by default): the lean
   instance the bench times, 8192 chains in one launch, against the C oracle on 64 chains sampled
@@ -33,6 +39,50 @@ def _c3(sec11, chains, *, offset=0, trace=0):
     run = FlipRun(FlipGraph(sec11), np.broadcast_to(a0, (chains, sec11.n)), cfg,
                   bases=np.full(chains, G.SEC11_MU))
     return run, a0, (lo, hi)
+
+
+def test_c2_production_shape_against_oracle(gpu, cref):
+    """The headline launch exactly as bench.py issues it (its Workload("c2"), its seed, one
+    100,000-step launch of 4096 chains), the kernel name asserted, 48 sampled chains against the
+    C oracle.  The oracle chains run on a thread pool (ctypes releases the GIL; fr_run keeps no
+    global state)."""
+    from concurrent.futures import ThreadPoolExecutor
+    import bench
+    W = bench.Workload("c2")
+    assert W.chains == 4096 and W.seed == 0x5EED0002 and W.k == 2 and W.pct == 0.1
+    C, steps = W.chains, 100000
+    spec = W.spec
+    inits = np.stack([W.init_of(g) for g in range(C)])
+    bases = np.asarray([W.base_of(g) for g in range(C)])
+    _, (lo, hi) = G.population_bounds(int(spec.pop.sum()), W.k, W.pct)
+    cfg = RunConfig(k=2, labels=(-1, 1), proposal=W.proposal, seed=W.seed, pop_lo=lo, pop_hi=hi, stream="node")
+    run = FlipRun(FlipGraph(spec), inits, cfg, bases=bases)
+    run.steps(steps)
+    name = run.kernel_name()
+    assert "flip2_kernel<8, 4, false, false, false, false>" in name, name
+    st, state = run.stats(), run.state()
+    assert (st["steps"] == steps).all() and not st["stuck"].any()
+    # 32 chains spread over the ids + one chain of each (base 6.96 / 10) x alignment configuration,
+    # placed in the upper half of the id range
+    spread = set(np.linspace(0, C - 1, 32).astype(np.int64).tolist())
+    slow = {2040 + 30 * j + 10 * al + b for j, (al, b) in enumerate((al, b) for al in range(3) for b in (8, 9))}
+    slow |= {C - 1 - ((C - 1 - g) % 30) for g in (8, 9, 18, 19, 28, 29)}   # the same six near the top
+    sample = sorted(spread | slow)[:48]
+    assert {(W.base_of(g), W.plan_of(g)) for g in sample} >= {(W.bases[b], al) for b in (8, 9) for al in range(3)}
+    l1 = G.log1mp_table(spec.n, 2)
+
+    def ref(g):
+        return g, cref.run(spec, inits[g], base=bases[g], pop_lo=lo, pop_hi=hi, seed=W.seed, chain_id=g,
+                           n_steps=steps, log1mp=l1)
+
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        refs = dict(ex.map(ref, sample))
+    for g in sample:
+        r = refs[g]
+        assert np.array_equal(state[g], r["final"]), g
+        for key in STAT_KEYS:
+            assert int(st[key][g]) == int(r["stats"][key]), (g, key, W.base_of(g))
+    run.close()
 
 
 def test_c3_production_shape_against_oracle(gpu, cref, sec11):

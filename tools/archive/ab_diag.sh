@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of prebuilt libraries (abl/*.so) on the C2 probe with a given diagnostics mask:
-#   DIAG=15 REP=2 bash tools/ab_diag.sh lib1.so lib2.so ...
+#   DIAG=15 REP=2 bash tools/archive/ab_diag.sh lib1.so lib2.so ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 for rep in $(seq 1 ${REP:-2}); do

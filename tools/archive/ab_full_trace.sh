@@ -2,7 +2,7 @@
 # Full-diagnostics instance variants on the C2 probe (diag 31 = waits, histograms, cut_times,
 # flips, event log; 4096 chains x 100,000 steps, 3 launches) under rocprofv3 --kernel-trace
 # --stats: flip kernel and tally_reduce means per library.
-#   bash tools/ab_full_trace.sh <tag> abl/x.so ...
+#   bash tools/archive/ab_full_trace.sh <tag> abl/x.so ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp FC_PROBE_DIAG=${DIAG:-31} FC_PROBE_EVCAP=100001
 TAG=$1; shift

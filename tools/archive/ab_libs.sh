@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of prebuilt library variants on the C2 probe (full 100,000-step launches):
-#   bash tools/ab_libs.sh <tag> lib1.so lib2.so ...
+#   bash tools/archive/ab_libs.sh <tag> lib1.so lib2.so ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 TAG=$1; shift

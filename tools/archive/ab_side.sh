@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of prebuilt library variants on a side workload (tools/probe_side.py):
-#   WL=c4 bash tools/ab_side.sh <tag> lib1.so lib2.so ...
+#   WL=c4 bash tools/archive/ab_side.sh <tag> lib1.so lib2.so ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 TAG=$1; shift

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of launch tunings on one library (C2 probe, 4096 chains x 100,000 steps):
-#   LIB=abl/x.so REP=2 bash tools/ab_tune.sh "" "nsub=8" ...
+#   LIB=abl/x.so REP=2 bash tools/archive/ab_tune.sh "" "nsub=8" ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 for rep in $(seq 1 ${REP:-2}); do

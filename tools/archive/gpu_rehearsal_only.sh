@@ -1,7 +1,7 @@
 #!/bin/bash
 # Two-rank rehearsals on one GPU (bench.py --gpus 2 launching its own ranks, gloo, both on
 # device 0) against one rank holding the same global chains: C2 and C3, reduced statistics
-# compared by tools/rehearsal_check.py.  (The rehearsal steps of tools/gpu_r04a.sh.)
+# compared by tools/rehearsal_check.py.  (The rehearsal steps of tools/archive/gpu_r04a.sh.)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"

@@ -1,5 +1,5 @@
 """Where the full-diagnostics leg's per-launch frame-series time goes (bench.py's loop, C2 full
-diagnostics + event log, 4096 chains x 100,000 steps): python tools/probe_series.py [iters]"""
+diagnostics + event log, 4096 chains x 100,000 steps): python tools/archive/probe_series.py [iters]"""
 import os
 import sys
 import time
