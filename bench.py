@@ -217,14 +217,18 @@ def resident_chains(fg, W, device: int = 0, flags: int = 0, tune=None) -> int:
     return cus * max(1, min(160 * 1024 // lds, 16))
 
 
-def measured_traffic(wname: str, kname: str, chains: int, chain_steps: int, root: str = ROOT):
+def measured_traffic(wname: str, kname: str, chains: int, chain_steps: int, root: str = ROOT, build_id: str = ""):
     """HBM bytes per launch of this kernel at this launch shape, from the separate rocprofv3
     FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md HBM section: (2 FETCH_SIZE + WRITE_SIZE)
     KiB): profiles/pmc_traffic.json for C2, the newest profiles/r*_side_pmc_<workload>.json for the
-    k > 2 side lines.  Returns (bytes, profile) or (None, None) when none matches."""
+    k > 2 side lines.  A kernel name does not identify a revision, so a summary counts only when
+    it records this run's library build id (as measured_l2).  Returns (bytes, profile,
+    stale) -- (None, None, stale) when none matches, ``stale`` naming the newest summary of the
+    same kernel and shape that was refused for its build id (or None)."""
     prof = os.path.join(root, "profiles")
     files = [os.path.join(prof, "pmc_traffic.json")] if wname == "c2" else \
         sorted(glob.glob(os.path.join(prof, f"r*_side_pmc_{wname}.json")), reverse=True)
+    stale = None
     for fn in files:
         try:
             tj = json.load(open(fn))
@@ -233,8 +237,12 @@ def measured_traffic(wname: str, kname: str, chains: int, chain_steps: int, root
         if (tj.get("chains") == chains and tj.get("chain_steps") == chain_steps
                 and tj.get("workload", "c2") == wname and kname in str(tj.get("kernel"))
                 and tj.get("hbm_bytes_per_launch")):
-            return tj["hbm_bytes_per_launch"], "profiles/" + os.path.basename(fn)
-    return None, None
+            if build_id and tj.get("build_id") == build_id:
+                return tj["hbm_bytes_per_launch"], "profiles/" + os.path.basename(fn), None
+            if stale is None:
+                stale = {"profile": "profiles/" + os.path.basename(fn), "build_id": tj.get("build_id"),
+                         "hbm_bytes_per_launch": tj["hbm_bytes_per_launch"]}
+    return None, None, stale
 
 
 def measured_l2(wname: str, kname: str, chains: int, chain_steps: int, kernel_ms: float, build_id: str = ""):
@@ -501,7 +509,10 @@ def cpu_baseline(seconds: float, cores: int, wname: str = "c2", kind: str = "nat
                "random.choice over the (node, district) pairs of slow_reversible_propose, grid_chain_sec11.py:128 "
                "over :151-153")
             + ", random() at :179, np.random.geometric at :148, gerrychain-0.2 Partition / cut_edges / Dijkstra "
-            "contiguity)" if kind == "native" else
+            "contiguity" + ("; where 1 - p rounds to 1.0 in double (C4 / C5: N^k beyond 2^53 |B|) its wait is "
+                            "saturated at 2^62 like the C oracle's and the device's, where numpy's geometric gives "
+                            "INT64_MIN -- sum_wait parity unpinned there" if Workload(wname).k > 2 else "")
+            + ")" if kind == "native" else
             "gerrychain-0.2-faithful Python restatement on the canonical Philox stream "
             "(oracle/flipref.py GcFaithfulChain)")
     return {"value": props / wall, "unit": "proposals/s", "cores": cores, "kind": "port",
@@ -545,6 +556,96 @@ def c_oracle_allcores(seconds: float, cores: int, wname: str = "c2"):
                       f"{seconds:.0f} s each"}
 
 
+def recom_leg(args) -> dict:
+    """Side line ``--workload recom``: the reference's ``tree_proposal`` (partial(recom,
+    pop_col="population", pop_target=ideal, epsilon=0.05, node_repeats=1), grid_chain_sec11.py:328-335)
+    on sec11, k = 2, the population Validator (0.1), always_accept; 4096 chains per GPU, one launch =
+    ``--chain-steps`` ReCom steps per chain (default here 20).  Device time from HIP events on the run's
+    stream; the roofline prices each spanning tree's algorithmic bytes -- every adjacency entry read
+    once (4 B x 2E), a weight per edge (4 B x E), the tree's parent and subtree population per node
+    (8 B x n) and the relabelled assignment (1 B x n) -- against the LDS aggregate (the chain's
+    working set is LDS-resident, fc_recom.hip).  CPU baseline: oracle/recomref.c, one process per
+    usable CPU."""
+    import torch
+    from flipcomplexityempirical_amd import _lib
+    from flipcomplexityempirical_amd import graphs as G
+    from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
+    spec = G.sec11_graph()
+    C = args.chains or 4096
+    S = args.chain_steps
+    plans = [spec.assignment_array(G.sec11_plan(al, spec.nodes), [-1, 1]) for al in range(3)]
+    inits = np.stack([plans[c % 3] for c in range(C)])
+    _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
+    seed = SEED + 0x10
+    cfg = RunConfig(proposal=_lib.FC_PROPOSE_RECOM, seed=seed, pop_lo=lo, pop_hi=hi, base=1.0,
+                    recom_pop_target=spec.n / 2, recom_epsilon=0.05, recom_node_repeats=1, diag_mask=0)
+    run = FlipRun(FlipGraph(spec), inits, cfg)
+    for _ in range(max(1, args.warmup)):
+        run.steps(S)
+    run.sync()
+    torch.cuda.synchronize()
+    run.timings()
+    s0 = run.stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run.steps(S)
+    run.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ms = run.timings()
+    s1 = run.stats()
+    steps = float((s1["steps"] - s0["steps"]).sum())
+    trees = float((s1["bfs_levels"] - s0["bfs_levels"]).sum())
+    roots = float((s1["bfs_calls"] - s0["bfs_calls"]).sum())
+    kms = float(ms.mean())
+    tree_bytes = 4 * 2 * spec.n_edges + 4 * spec.n_edges + 8 * spec.n + spec.n
+    alg = tree_bytes * trees / args.steps
+    lds_peak = LDS_READ_BPC[4] * LDS_CUS * LDS_CLK_GHZ  # b32 gathers
+    out = {"metric": "recom steps/sec, sec11 40x40 k=2 (tree_proposal of grid_chain_sec11.py:328-335)",
+           "value": steps / dt, "unit": "steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "dtype": "int8", "data": "synthetic",
+           "config": {"workload": "ReCom on sec11 (N=1596), k=2, pop tol 0.1, always_accept, "
+                                  f"{C} chains, {S} ReCom steps per chain per launch", "chains_per_gpu": C,
+                      "chain_steps_per_launch": S},
+           "kernel": run.kernel_name(), "kernel_ms": kms, "steps_per_s_kernel": steps / (ms.sum() * 1e-3),
+           "trees_per_step": trees / steps, "roots_per_step": roots / steps,
+           "build_id": _lib.build_id(),
+           "roofline": {"bound": "lds", "achieved": alg / (kms * 1e-3) / 1e9, "peak": lds_peak, "unit": "GB/s",
+                        "frac": alg / (kms * 1e-3) / 1e9 / lds_peak, "traffic": None,
+                        "alg_bytes_per_tree": tree_bytes,
+                        "note": "per spanning tree: adjacency 4 B x 2E + edge weight 4 B x E + parent / subtree "
+                                "population 8 B x n + assignment 1 B x n, against the LDS b32 aggregate "
+                                "(MI355X_MICROARCH.md §LDS: 128 B/clk/CU x 256 CUs x 2.4 GHz)"}}
+    run.close()
+    if not args.no_cpu_baseline:
+        cores, share = host_cpu_share()
+        from concurrent.futures import ProcessPoolExecutor
+        with ProcessPoolExecutor(max_workers=cores) as ex:
+            res = list(ex.map(_recom_cpu_worker, [(i, cores, min(args.cpu_seconds, 10.0), seed) for i in range(cores)]))
+        out["cpu_baseline"] = {"value": sum(r[0] for r in res) / max(r[1] for r in res), "unit": "steps/s",
+                               "cores": cores, "kind": "port", **share,
+                               "sample": f"oracle/recomref.c, {cores} processes, chains of 50 steps from the start "
+                                         f"plans for {min(args.cpu_seconds, 10.0):.0f} s each"}
+    return out
+
+
+def _recom_cpu_worker(args):
+    i, stride, seconds, seed = args
+    sys.path.insert(0, ROOT)
+    from flipcomplexityempirical_amd import graphs as G
+    from oracle.flipref import recom_run
+    spec = G.sec11_graph()
+    plans = [spec.assignment_array(G.sec11_plan(al, spec.nodes), [-1, 1]) for al in range(3)]
+    _, (lo, hi) = G.population_bounds(spec.n, 2, 0.1)
+    t0, n, c = time.perf_counter(), 0, i
+    while time.perf_counter() - t0 < seconds:
+        r = recom_run(spec, plans[c % 3], k=2, pop_target=spec.n / 2, epsilon=0.05, pop_lo=lo, pop_hi=hi,
+                      seed=seed, chain_id=c, n_steps=50)
+        n += r["stats"]["steps"]
+        c += stride
+    return n, time.perf_counter() - t0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -552,7 +653,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chain-steps", type=int, default=100000)
     ap.add_argument("--chains", type=int, default=0, help="chains per GPU (0: the workload's)")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "recom"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep-replicas", type=int, default=1,
@@ -593,6 +694,13 @@ def main():
     dist, rank, world, local_rank = _dist()
     from flipcomplexityempirical_amd import _lib as _lib0
     _lib0.load(allow_variant=args.allow_variant)
+    if args.workload == "recom":  # side line, one GPU
+        if world > 1:
+            raise SystemExit("bench.py --workload recom is a one-GPU side line")
+        if args.chain_steps == 100000:
+            args.chain_steps = 20
+        print(json.dumps(recom_leg(args)), flush=True)
+        return
     import torch
     from flipcomplexityempirical_amd import graphs as G
     from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig, parse_tune, pin_host, unpin_host
@@ -811,6 +919,7 @@ def main():
             for b_ in cp_buf.values():
                 unpin_host(b_)
         kf = D.allreduce_max(float(rf.timings().mean()), dist, dev)
+        diag_paths = rf.diag_paths()
         f1 = rf.stats()
         arrays = {}
         if full & _lib.FC_DIAG_HIST:
@@ -830,6 +939,9 @@ def main():
         full_out = {"value": pf / (dtf - t_series - t_acf), "unit": "proposals/s", "launches": n_full,
                     "value_with_frame_series_on_host": pf / dtf if series else None,
                     "kernel": rf.kernel_name(), "kernel_ms": kf,
+                    "diag_paths": dict(diag_paths, note="fc_run_diag_paths: tally-log entries per chain granted / "
+                                       "asked for (granted below asked: chains may apply tallies by atomics), and "
+                                       "whether the change points ran one staged pass (1) or two (0); same outputs"),
                     "diag": ("waits + accepted-flip log -> |cut| autocorrelation and hitting time on the device "
                              "(BASELINE config 4)" if c4diag else
                              "waits + cut/|B| histograms + per-edge cut_times + per-node flips"
@@ -892,7 +1004,8 @@ def main():
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     acc_pp = per_launch_acc / per_launch_props if per_launch_props else 0.0
     lds_peak = lds_mix_peak_gbs(W.rmix, W.wmix, acc_pp)
-    traffic, traffic_src = measured_traffic(args.workload, kname, C, args.chain_steps)
+    traffic, traffic_src, traffic_stale = measured_traffic(args.workload, kname, C, args.chain_steps,
+                                                           build_id=_lib.build_id())
     levels = roofline_levels(W, per_launch_props, per_launch_acc, kernel_ms, traffic)
     l1l2 = measured_l2(args.workload, kname, C, args.chain_steps, kernel_ms, _lib.build_id())
     out = {
@@ -941,8 +1054,9 @@ def main():
                                   "half; 256 CUs, 2.4 GHz; reads %s B, writes %s B per accept, %.3f accepts per "
                                   "proposal), the round-3 pricing" % (W.rmix, W.wmix, acc_pp),
                      "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of "
-                                     "this kernel and run shape (%s; gfx950 FETCH_SIZE doubled)"
-                                     % (traffic_src or "none recorded for it"),
+                                     "this kernel, run shape and library build (%s; gfx950 FETCH_SIZE doubled)"
+                                     % (traffic_src or "none recorded for this build"),
+                     "traffic_stale_build": traffic_stale,
                      "kernel": kname,
                      "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": alg_bytes,

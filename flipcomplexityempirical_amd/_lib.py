@@ -41,7 +41,8 @@ EXPORTED = [
     "fc_run_read_edges", "fc_run_read_flips", "fc_run_read_flips_exact", "fc_run_read_wait_expected",
     "fc_run_read_events", "fc_run_series_reset", "fc_run_autocorr",
     "fc_run_frame_series", "fc_run_frame_series_changes", "fc_host_register", "fc_host_unregister",
-    "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_nb_width", "fc_run_destroy",
+    "fc_run_kernel_name", "fc_run_n_chains", "fc_run_chain_lds_bytes", "fc_run_nb_width", "fc_run_diag_paths",
+    "fc_run_destroy",
     "fc_device_count", "fc_device_pci_id", "fc_last_error", "fc_build_flags", "fc_build_id",
 ]
 
@@ -214,6 +215,7 @@ def load(build_if_missing: bool = True, allow_variant: bool = False):
     L.fc_run_n_chains.restype = i32
     L.fc_run_chain_lds_bytes.argtypes = [vp]
     L.fc_run_chain_lds_bytes.restype = i32
+    L.fc_run_diag_paths.argtypes = [vp, _P(i64), _P(i64), _P(i32)]
     L.fc_run_nb_width.argtypes = [vp]
     L.fc_run_nb_width.restype = i32
     L.fc_device_pci_id.argtypes = [i32, ctypes.c_char_p, i32]

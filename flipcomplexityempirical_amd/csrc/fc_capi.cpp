@@ -50,6 +50,8 @@ struct fc_run {
     uint32_t *d_tl = nullptr;
     int64_t *d_tl_len = nullptr, *d_tl_t0 = nullptr;
     int64_t tl_cap = 0;
+    int64_t tl_want = 0;           // entries per chain the last launch asked for (tl_cap: granted)
+    int32_t series_staged = -1;    // last fc_run_frame_series_changes: 1 one staged pass, 0 two passes
     int64_t *d_num_flips = nullptr, *d_part_sum = nullptr, *d_last_flipped = nullptr;
     int64_t *d_flip_count = nullptr, *d_occ_acc = nullptr, *d_last_accept = nullptr;  // FC_DIAG_FLIPS_EXACT
     int32_t *d_popk = nullptr;
@@ -306,6 +308,14 @@ int32_t fc_run_n_chains(const fc_run *r) { return r ? r->n_chains : 0; }
 int32_t fc_run_chain_lds_bytes(const fc_run *r) { return r ? r->chain_lds_bytes : 0; }
 
 int32_t fc_run_nb_width(const fc_run *r) { return r ? r->nb_w : 0; }
+
+int fc_run_diag_paths(const fc_run *r, int64_t *tally_log_cap, int64_t *tally_log_wanted, int32_t *series_staged) {
+    if (!r || !tally_log_cap || !tally_log_wanted || !series_staged) return fail(FC_ERR_ARG, "fc_run_diag_paths: null argument");
+    *tally_log_cap = r->tl_cap;
+    *tally_log_wanted = r->tl_want;
+    *series_staged = r->series_staged;
+    return FC_OK;
+}
 
 int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, const int8_t *init_assign,
                   const double *bases, fc_run **out) {
@@ -1009,6 +1019,7 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
         const int64_t steps1 = std::min(chunk, n_steps);
         int64_t want = steps1 + steps1 / 8 + 256;
         if (r->p.flags & FC_FLAG_TALLY_LOG_SMALL) want = std::min<int64_t>(want, 64);
+        r->tl_want = want;
         if (want > r->tl_cap) {
             size_t free_b = 0, total_b = 0;
             HIP_TRY(hipMemGetInfo(&free_b, &total_b));
@@ -1671,6 +1682,7 @@ int fc_run_frame_series_changes(fc_run *r, int32_t c0, int32_t nc, int32_t n_fra
         }
         staged = want <= r->fc_stage_cap;
     }
+    if (!query) r->series_staged = staged ? 1 : 0;
     const size_t stn = r->fc_stage_cap;  // staging: slope at d_st_sa, angle at d_st_sa + stn
     int e;
     if (staged)

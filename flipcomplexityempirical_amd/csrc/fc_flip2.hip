@@ -275,7 +275,12 @@ int launch_tally_reduce(const KParams &p, int ring_max, void *stream) {
     auto bytes = [&](int a) -> size_t {
         return 8 * (size_t)(a == 0 ? p.n_edges + 1 : a == 1 ? p.n + 1 : a == 2 ? p.n_edges : p.n);
     };
-    constexpr size_t kPass = 160 * 1024, kMaxLds = 160 * 1024;
+    // the device's LDS per workgroup (gfx950: 160 KiB), queried, not assumed
+    int dev = 0, optin = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || optin <= 0)
+        optin = 65536;
+    const size_t kPass = (size_t)optin, kMaxLds = (size_t)optin;
     std::vector<std::pair<uint32_t, size_t>> passes;
     uint32_t gmask = 0;
     for (int a = 0; a < kTrArrays; ++a) {
@@ -297,20 +302,24 @@ int launch_tally_reduce(const KParams &p, int ring_max, void *stream) {
     }
     if (passes.empty()) passes.emplace_back(0u, 0);
     for (size_t i = 0; i < passes.size(); ++i) {
-        const size_t lds = passes[i].second;
-        const uint32_t g = i == 0 ? gmask : 0u;
+        size_t lds = passes[i].second;
+        uint32_t lmask = passes[i].first, g = i == 0 ? gmask : 0u;
         const int last = i + 1 == passes.size() ? 1 : 0;
-        if (ring_max <= 8) {
-            if (lds > 65536)
-                (void)hipFuncSetAttribute((const void *)tally_reduce_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(tally_reduce_kernel<8>, dim3(p.n_chains), dim3(1024), lds, (hipStream_t)stream, p,
-                               passes[i].first, g, last);
-        } else {
-            if (lds > 65536)
-                (void)hipFuncSetAttribute((const void *)tally_reduce_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(tally_reduce_kernel<16>, dim3(p.n_chains), dim3(1024), lds, (hipStream_t)stream, p,
-                               passes[i].first, g, last);
+        const void *fn = ring_max <= 8 ? (const void *)tally_reduce_kernel<8> : (const void *)tally_reduce_kernel<16>;
+        if (lds > 65536 &&
+            hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+            // the device refuses this much dynamic LDS: the pass's arrays take the global atomics
+            (void)hipGetLastError();
+            g |= lmask;
+            lmask = 0;
+            lds = 0;
         }
+        if (ring_max <= 8)
+            hipLaunchKernelGGL(tally_reduce_kernel<8>, dim3(p.n_chains), dim3(1024), lds, (hipStream_t)stream, p,
+                               lmask, g, last);
+        else
+            hipLaunchKernelGGL(tally_reduce_kernel<16>, dim3(p.n_chains), dim3(1024), lds, (hipStream_t)stream, p,
+                               lmask, g, last);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }

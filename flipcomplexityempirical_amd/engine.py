@@ -535,6 +535,15 @@ class FlipRun:
         bounds = np.concatenate([[t0], ev["t"], [T + 1]]).astype(np.int64)
         return np.repeat(np.asarray(values)[:ev.size + 1], np.diff(bounds))
 
+    def diag_paths(self) -> Dict[str, int]:
+        """The paths the memory-dependent diagnostics took (``fc_run_diag_paths``): tally-log
+        entries per chain granted / asked for, and whether the last change-point call was staged."""
+        cap, want, staged = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
+        check(_lib.load().fc_run_diag_paths(self.handle, ctypes.byref(cap), ctypes.byref(want), ctypes.byref(staged)),
+              "fc_run_diag_paths")
+        return {"tally_log_cap": int(cap.value), "tally_log_wanted": int(want.value),
+                "series_staged": int(staged.value)}
+
     def nb_width(self) -> int:
         """Entries of a chain's |B| histogram row (``fc_run_nb_width``): n + 1, or the largest
         pair count + 1 with ``FC_FLAG_NB_PAIRS``."""

@@ -408,6 +408,13 @@ int32_t fc_run_chain_lds_bytes(const fc_run *r);
 /* Entries of a chain's |B| histogram row and of the log1mp table: n + 1, or with
  * FC_FLAG_NB_PAIRS (k > 2) sum_u min(deg u, k - 1) + 1, the largest pair count + 1. */
 int32_t fc_run_nb_width(const fc_run *r);
+/* Which paths the memory-dependent diagnostics took (outputs are the same either way):
+ * the k = 2 tally log's entries per chain granted (*tally_log_cap; 0 = none, every tally by
+ * global atomics) against those the last launch asked for (*tally_log_wanted: a granted size
+ * below it means chains may have filled the log and applied the rest by atomics), and whether
+ * the last fc_run_frame_series_changes ran one staged pass (*series_staged = 1), the two-pass
+ * form (0) or none yet (-1). */
+int fc_run_diag_paths(const fc_run *r, int64_t *tally_log_cap, int64_t *tally_log_wanted, int32_t *series_staged);
 void fc_run_destroy(fc_run *r);
 
 int fc_device_count(int32_t *n);

@@ -72,6 +72,7 @@ traffic = {"round": tag, "kernel": check["kernel"], "chains": bench["config"]["c
            "FETCH_SIZE_KiB_per_launch": fetch, "WRITE_SIZE_KiB_per_launch": write,
            "launches": {k: len(v) for k, v in vals.items()},
            "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
+           "build_id": bench.get("build_id"),  # the library the counters measured (bench.measured_traffic)
            "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md HBM section)"}
 json.dump(traffic, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
 json.dump(traffic, open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w"), indent=1)
@@ -127,7 +128,9 @@ for w in ("c3", "c4", "c5"):  # counters of the k > 2 instances
     side["chain_steps"] = 20000
     p = os.path.join(src, f"side_{w}.json")
     if os.path.exists(p):
-        side["chains"] = json.loads(open(p).read().strip().splitlines()[-1])["config"]["chains_per_gpu"]
+        line = json.loads(open(p).read().strip().splitlines()[-1])
+        side["chains"] = line["config"]["chains_per_gpu"]
+        side["build_id"] = line.get("build_id")
     hb = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         rows = [r for r in flip_rows(os.path.join(src, f"side_pmc_{w}_{c}", "pmc_counter_collection.csv"))
