@@ -251,3 +251,18 @@ def test_frame_series_changes_at_full_c2_size(gpu, sec11):
             assert np.array_equal(ch["t"][lo_:hi_], t_all[keep]), c
             assert np.array_equal(ch["slope"][lo_:hi_].view(np.int64), s[keep]), c
             assert np.array_equal(ch["angle"][lo_:hi_].view(np.int64), a[keep]), c
+            if c in (sample[3], sample[-1]):
+                # the per-event series itself against a reference that shares no kernel
+                # code -- the host replay of the chain's first 1500 events through the oracle's
+                # boundary_slope and the loop body (:371-394), from the launch's start state
+                ev = run.events(c)[:1500]
+                a_h = inits[c].copy()
+                for j in range(ev.size + 1):
+                    if j:
+                        a_h[int(ev[j - 1]["v"])] = ev[j - 1]["target"]
+                    temp = boundary_slope(cut_edge_labels(sec11, a_h), "sec11")
+                    assert int(dense["n_cut"][0, j]) == len(temp), (c, j)
+                    if len(temp) >= 2:
+                        s_ref, a_ref = slope_angle(temp)
+                        assert dense["slope"][0, j] == s_ref, (c, j)
+                        assert abs(dense["angle"][0, j] - a_ref) <= ANGLE_TOL, (c, j)
