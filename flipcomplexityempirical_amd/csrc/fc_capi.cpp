@@ -451,7 +451,10 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
         auto per_cu = [](int b) { return std::min(16, 160 * 1024 / (((b + 15) / 16 * 16 + 1279) / 1280 * 1280)); };
         const int mf = p->tune_multi_flip;
         r->mf_marks = 0;
-        if (!recom && k > 2 && r->dgraph && mf != -1) {
+        // FC_FLAG_NB_PAIRS runs take the one-flip-at-a-time commit: the multi-flip pass counts
+        // |B| as nodes only (its pair count would cost the C5 instance the register that keeps
+        // three waves per SIMD)
+        if (!recom && k > 2 && r->dgraph && mf != -1 && !nb_pairs) {
             // exact marks (a byte per node) when they cost no residency, else the hashed set
             const bool fits = per_cu(base_b + r->npad) >= per_cu(base_b + fc::hb_bytes(R));
             r->mf_marks = mf == 2 ? 1 : mf == 3 ? 2 : (fits ? 2 : 1);

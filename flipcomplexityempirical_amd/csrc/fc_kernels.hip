@@ -860,12 +860,6 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                         if (app && nb_m && nfn_m != old_m) pkb[um] = (uint8_t)(au_m | ((nfn_m < 7 ? nfn_m : 7) << 5));
                         const bool ent_m = app && nb_m && old_m == 0 && nfn_m > 0;
                         const bool lev_m = app && nb_m && old_m > 0 && nfn_m == 0;
-                        // FC_FLAG_NB_PAIRS: |B| counts (node, district) pairs -- each flip's change
-                        // is its neighbours' nf changes plus its own node's, summed over lane groups
-                        int pscan = 0;
-                        if (p.nb_pairs)
-                            pscan = wave_scan_incl((app && nb_m ? nfn_m - old_m : 0) +
-                                                   (app && ge == 0 ? nf_af - nf_bf : 0));
                         // the slots up to the last flip applied: verdict bits, |cut| / |B| after each flip
                         const int fl = nA_ == nF ? f_last : select_bit64(FM, nA_ - 1);
                         if (prop && lane >= f && lane <= fl) st |= bits;
@@ -882,15 +876,14 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                                 my_cs = rk == g ? csum : my_cs;
                             }
                         const uint64_t ENT = __ballot(ent_m), LEV = __ballot(lev_m);
-                        const int pupto = p.nb_pairs ? __shfl(pscan, ((rk + 1) * RMAX - 1) & 63) : 0;
                         if (((FM >> lane) & 1ull) && rk < nA_) {
                             const uint64_t upto = bits_below((rk + 1) * RMAX);
                             st |= ST_VS | ST_AC;
                             cut_after = cut + my_cs;
-                            nb_after = p.nb_pairs ? nb + pupto : nb + __popcll(ENT & upto) - __popcll(LEV & upto);
+                            nb_after = nb + __popcll(ENT & upto) - __popcll(LEV & upto);
                         }
                         cut += csum;
-                        nb += p.nb_pairs ? rl32(pscan, 63) : __popcll(ENT) - __popcll(LEV);
+                        nb += __popcll(ENT) - __popcll(LEV);
                         rem -= __popcll(VAL & lane_range(f, fl + 1));
                         last_flip = rl32(v, fl);
                         compiler_fence();

@@ -98,7 +98,8 @@ extern "C" {
                                     k > 2 driver running slow_reversible_propose (:117-130)
                                     registers as "b_nodes", instead of the nodes of b_nodes_bi
                                     (:155-156).  The histogram and log1mp then have
-                                    fc_run_nb_width entries; no-op for k = 2                     */
+                                    fc_run_nb_width entries; no-op for k = 2.  Such runs commit
+                                    one flip at a time (tune_multi_flip has no effect)           */
 
 typedef struct fc_graph fc_graph;
 typedef struct fc_run fc_run;

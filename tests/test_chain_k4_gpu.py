@@ -108,10 +108,10 @@ def test_k4_driver_loop_matches_fast_path_and_oracle(gpu, cref, base, pop1, chai
     assert np.array_equal(ref["final"], fin)
 
 
-def test_k4_pairs_multi_flip_launches_against_oracle(gpu, cref):
+def test_k4_pairs_launches_against_oracle(gpu, cref):
     """FC_FLAG_NB_PAIRS through the lean and full k > 2 instances at production width (256 chains,
-    the multi-flip commit on, the pair count changed by several flips per pass), in three
-    launches, against the oracle per chain; and the node-count default stays the C3 stream."""
+    bases with high and low acceptance), in three launches, against the oracle per chain.  Such
+    runs commit one flip at a time (the multi-flip pass counts |B| as nodes only)."""
     from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
     sec11 = G.sec11_graph()
     k = 4
@@ -126,6 +126,7 @@ def test_k4_pairs_multi_flip_launches_against_oracle(gpu, cref):
         assert run.nb_width() == W
         for n in (700, 1, 1299):
             run.steps(n)
+        assert run.kernel_name().endswith(", 0>"), run.kernel_name()  # no multi-flip instance
         st, fin = run.stats(), run.state()
         nh = run.hist()[1] if diag & _lib.FC_DIAG_HIST else None
         for c in range(0, 256, 17):
