@@ -566,7 +566,6 @@ def recom_leg(args) -> dict:
     (8 B x n) and the relabelled assignment (1 B x n) -- against the LDS aggregate (the chain's
     working set is LDS-resident, fc_recom.hip).  CPU baseline: oracle/recomref.c, one process per
     usable CPU."""
-    import torch
     from flipcomplexityempirical_amd import _lib
     from flipcomplexityempirical_amd import graphs as G
     from flipcomplexityempirical_amd.engine import FlipGraph, FlipRun, RunConfig
@@ -583,14 +582,12 @@ def recom_leg(args) -> dict:
     for _ in range(max(1, args.warmup)):
         run.steps(S)
     run.sync()
-    torch.cuda.synchronize()
     run.timings()
     s0 = run.stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run.steps(S)
     run.sync()
-    torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     ms = run.timings()
     s1 = run.stats()
