@@ -149,17 +149,29 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                         const int cx = comp[x];
                         if (cx < 0) continue;
                         const NodeRec<RMAX> r = G[x];
+                        // the node's ring edge ids (static, RMAX / 4 vector loads) and its ring
+                        // cells' components, every read issued before the first use (one at a time
+                        // behind each neighbour test before: a dependent L2 and LDS round trip per
+                        // edge); the keys are then formed by selects, without a branch per cell
+                        int4 er[RMAX / 4];
+                        const int4 *rp = (const int4 *)(p.ring_eid + (size_t)x * RMAX);
+#pragma unroll
+                        for (int q = 0; q < RMAX / 4; ++q) er[q] = rp[q];
                         const uint32_t nbr = (uint32_t)(r.meta >> kMetaNbrShift) & 0xffffu;
+                        int cyv[RMAX];
+#pragma unroll
+                        for (int j = 0; j < RMAX; ++j) cyv[j] = comp[ring_entry<RMAX>(r.ring, j)];
+#pragma unroll
+                        for (int j = 0; j < RMAX; ++j) asm volatile("" : "+v"(cyv[j]));
                         uint64_t bk = 0;
 #pragma unroll
                         for (int j = 0; j < RMAX; ++j) {
-                            if (!((nbr >> j) & 1u)) continue;
-                            const int y = ring_entry<RMAX>(r.ring, j);
-                            const int cy = comp[y];
-                            if (cy < 0 || cy == cx) continue;
-                            const uint32_t e = (uint32_t)p.ring_eid[(size_t)x * RMAX + j];
+                            const int4 eq = er[j >> 2];
+                            const int ej = (j & 3) == 0 ? eq.x : (j & 3) == 1 ? eq.y : (j & 3) == 2 ? eq.z : eq.w;
+                            const bool use = ((nbr >> j) & 1u) && cyv[j] >= 0 && cyv[j] != cx;
+                            const uint32_t e = (uint32_t)ej;
                             const uint64_t kk = ((splitmix64(key + (uint64_t)e) >> 32) << 32) | (0xffffffffu - e);
-                            bk = kk > bk ? kk : bk;
+                            bk = (use && kk > bk) ? kk : bk;
                         }
                         if (bk) atomicMax((unsigned long long *)&best[cx], (unsigned long long)bk);
                     }
