@@ -46,7 +46,7 @@ using namespace dev;
 // as KM = 0 when the district-graph rule decides every proposal (p.dgraph): no search code.
 // RMAX = 8: at most 128 VGPRs, four waves per SIMD (C3's 8192 chains per GPU run in two
 // rounds of waves instead of three: 1.46e9 against 1.35e9 proposals/s; a handful of VGPRs
-// spill, which costs C4's LDS-limited launch 2 %)
+// spill; C4's LDS-limited launch with three waves' budget and no spills: 25.4 against 25.1 ms)
 // MF (KM = 3): the multi-flip commit below, in an instance of its own so that runs without it
 // keep the smaller code
 #ifndef FC_K_WAVES8
@@ -551,7 +551,19 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
             // take the flips one by one in slot order, and the first flip that changes an adjacency
             // bit or the slot bound is the last one applied -- exactly the one-flip-at-a-time chain.
             if constexpr (KM == 3 && MF != 0) {
-                constexpr int kGrp = 64 / RMAX;  // flips per pass (one lane per ring cell)
+                constexpr int kGrp = 64 / RMAX;  // flips per pass, RMAX lanes each (one per ring cell)
+                // RMAX = 16 (MF = 1): the flips taken are packed by ring length instead (flip g owns
+                // the lanes [o_g, o_g + L_g)), up to kMaxF of them in 64 lanes -- on the Delaunay
+                // dual (rings of ~6) the four-flip cap ended 0.68 selections per pass of the slowest
+                // chains; on RMAX = 8 lattices the longer selection cost more than it saved
+                constexpr bool kPack = MF == 1 && RMAX == 16;
+                // RMAX = 8 (MF = 1): a taken flip that changes a later proposal's population verdict
+                // does not end the selection; every later slot's verdict is re-read under the
+                // populations after the flips taken before it (vcur), and the next candidate follows
+                // from it (C4: 0.39 selections per pass ended there; +6 % per launch.  On C5 the
+                // extra registers cost more than the 0.04-0.13 ends per pass it saves)
+                constexpr bool kReeval = MF == 1 && !kPack;
+                constexpr int kMaxF = kPack ? 16 : kGrp;
                 const uint64_t CANDM = __ballot(valid && acc) & lane_range(f, end);
                 if (__popcll(CANDM) >= 2) {
                     FC_PROF(21, 1);
@@ -561,7 +573,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                     int cutA = end;     // first slot whose view a taken flip changed (the batch ends there)
                     int cutP = kWave;   // first proposal whose population verdict changed
                     int dA = 0, dT = 0; // this slot's district populations moved by the taken flips
-                    const int gi = lane / RMAX, ge = lane % RMAX;
+                    int gi = lane / RMAX, ge = lane % RMAX;
+                    uint64_t S = 0;    // kPack: group starts (lane o_g of each flip taken)
+                    int cumL = 0;      // kPack: lanes the groups span
+                    bool cap_end = false;
                     // lane group g <- the g-th flip (slot order) of mask M: its data, and this lane's
                     // ring cell of it
                     int mg, vm, Am, Tm, um;
@@ -583,7 +598,7 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
         }                                                                                     \
         um = (int)((selm_ >> (16 * (ge & 1))) & 0xffffu);                                     \
     } while (0)
-                    int nT = kGrp;  // MF = 2: the first candidate sharing a neighbour with an earlier one
+                    int nT = kMaxF;  // MF = 2: the first candidate sharing a neighbour with an earlier one
                     bool nb_k = false;  // MF = 2: this lane's cell is a neighbour of its group's candidate
                     NodeRec<RMAX> ru;   // MF = 2: that neighbour's node record, loaded during the selection
                     if constexpr (MF == 2) {
@@ -602,13 +617,20 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                         nT = CL ? (int)(__builtin_ctzll(CL) / RMAX) : nK;
                     }
                     uint64_t CC = CANDM;
-                    for (; CC && nF < nT; CC &= CC - 1ull) {
+                    bool vcur = valid;  // kReeval: this slot's verdict after the flips taken before it
+                    while (CC && nF < nT) {
                         const int i = __builtin_ctzll(CC);
+                        CC &= CC - 1ull;
                         if (i >= cutA || i >= cutP) {
                             FC_PROF(i >= cutA ? 29 : 30, 1);
                             break;
                         }
                         if constexpr (MF == 1) {  // (statement order kept: hipcc spills 13 more VGPRs otherwise)
+                            const int Li = kPack ? max((int)rlu(Ln, i), 1) : RMAX;
+                            if (kPack && cumL + Li > kWave) {
+                                cap_end = true;
+                                break;
+                            }
                             const int vi = rl32(v, i);
                             const uint32_t pki = rlu(pk, i), nbri = rlu(pk2, i) >> 16;
                             const int Ai = (int)((pki >> 15) & 63u), Ti = (int)((pki >> 21) & 63u);
@@ -619,9 +641,9 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                             // its neighbours against the marks of the flips taken before it
                             uint32_t sel = rwi[0];
 #pragma unroll
-                            for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((ge >> 1) == k2) ? rwi[k2] : sel;
-                            const int ui = (int)((sel >> (16 * (ge & 1))) & 0xffffu);
-                            const bool isn = gi == 0 && ((nbri >> ge) & 1u);
+                            for (int k2 = 1; k2 < RMAX / 2; ++k2) sel = ((lane >> 1) == k2) ? rwi[k2] : sel;
+                            const int ui = (int)((sel >> (16 * (lane & 1))) & 0xffffu);
+                            const bool isn = lane < RMAX && ((nbri >> lane) & 1u);
                             if (nF > 0) {
                                 const bool clash = isn && ((hb[(ui & kHbMask) >> 5] >> (ui & 31)) & 1u);
                                 if (__any(clash)) {
@@ -632,6 +654,10 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                             if (isn) atomicOr(&hb[(ui & kHbMask) >> 5], 1u << (ui & 31));
                             FM |= 1ull << i;
                             ++nF;
+                            if constexpr (kPack) {
+                                S |= 1ull << cumL;
+                                cumL += Li;
+                            }
                             // later slots whose node is vi or has vi in its own ring (rings are symmetric)
                             bool stl = v == vi;
 #pragma unroll
@@ -643,8 +669,13 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                             dA += (av == Ti ? pvi : 0) - (av == Ai ? pvi : 0);
                             dT += (tgt == Ti ? pvi : 0) - (tgt == Ai ? pvi : 0);
                             const bool pok2 = (pa + dA - pv >= pop_lo) && (pb + dT + pv <= pop_hi);
-                            const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
-                            if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
+                            if constexpr (kReeval) {
+                                if (lane > i) vcur = prop && known && ok && pok2;
+                                CC = __ballot(vcur && acc) & lane_range(i + 1, end);
+                            } else {
+                                const uint64_t PM = __ballot(prop && lane > i && pok2 != popok);
+                                if (PM && __builtin_ctzll(PM) < cutP) cutP = __builtin_ctzll(PM);
+                            }
                         } else {
                             const int vi = rl32(v, i);
                             const uint32_t pki = rlu(pk, i);
@@ -668,12 +699,18 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                         }
                     }
                     if (MF == 2 && CC && nF == nT && nT < kGrp) FC_PROF(31, 1);
-                    if (CC && nF == kGrp) FC_PROF(28, 1);
+                    if (CC && (nF == kMaxF || cap_end)) FC_PROF(28, 1);
                     FC_STAMP(t_m1);
                     FC_PROF(23, t_m1 - t_m0);
                     const int f_last = 63 - __builtin_clzll(FM);
-                    const int nv = __popcll(VAL & lane_range(f, f_last + 1));
+                    const uint64_t VALc = kReeval ? __ballot(vcur) : VAL;
+                    const int nv = __popcll(VALc & lane_range(f, f_last + 1));
                     if constexpr (MF == 1) {  // the flips taken (mapped here: keeps the selection's registers)
+                        if constexpr (kPack) {
+                            const uint64_t upS = S & bits_below(lane + 1);
+                            gi = lane < cumL ? __popcll(upS) - 1 : kMaxF;
+                            ge = lane < cumL ? lane - (63 - __builtin_clzll(upS)) : 0;
+                        }
                         mg = gi < nF ? select_bit64(FM, gi) : f;
                         pkm = (uint32_t)__shfl((int)pk, mg);
                         pk2m = (uint32_t)__shfl((int)pk2, mg);
@@ -862,29 +899,42 @@ __global__ __launch_bounds__(256, (RMAX == 8 ? FC_K_WAVES8 : 1)) void flip_kerne
                         const bool lev_m = app && nb_m && old_m > 0 && nfn_m == 0;
                         // the slots up to the last flip applied: verdict bits, |cut| / |B| after each flip
                         const int fl = nA_ == nF ? f_last : select_bit64(FM, nA_ - 1);
-                        if (prop && lane >= f && lane <= fl) st |= bits;
+                        if (prop && lane >= f && lane <= fl) st |= kReeval ? (vcur ? ST_VS : (ok ? ST_IP : ST_IC)) : bits;
                         // flip of rank rk (slot order): |cut| after it = cut + the first rk+1 deltas
                         // (lane group g holds flip g's delta), |B| = nb + the entering / leaving
                         // neighbours of lane groups 0..rk
                         const int rk = count_below(FM);
                         const int dm = (int)((pk3m >> 16) & 0x3fu) - 32;
-                        int csum = 0, my_cs = 0;
+                        int csum = 0, my_cs = 0, my_up = 0;
+                        if constexpr (!kPack) {
 #pragma unroll
-                        for (int g = 0; g < kGrp; ++g)
-                            if (g < nA_) {
-                                csum += rl32(dm, g * RMAX);
+                            for (int g = 0; g < kGrp; ++g)
+                                if (g < nA_) {
+                                    csum += rl32(dm, g * RMAX);
+                                    my_cs = rk == g ? csum : my_cs;
+                                }
+                            my_up = (rk + 1) * RMAX;
+                        } else {
+                            uint64_t SS = S;
+                            for (int g = 0; g < nA_; ++g) {
+                                const int o = __builtin_ctzll(SS);
+                                SS &= SS - 1ull;
+                                csum += rl32(dm, o);
+                                const int nx = SS ? __builtin_ctzll(SS) : cumL;  // lanes of groups 0..g
                                 my_cs = rk == g ? csum : my_cs;
+                                my_up = rk == g ? nx : my_up;
                             }
+                        }
                         const uint64_t ENT = __ballot(ent_m), LEV = __ballot(lev_m);
                         if (((FM >> lane) & 1ull) && rk < nA_) {
-                            const uint64_t upto = bits_below((rk + 1) * RMAX);
+                            const uint64_t upto = bits_below(my_up);
                             st |= ST_VS | ST_AC;
                             cut_after = cut + my_cs;
                             nb_after = nb + __popcll(ENT & upto) - __popcll(LEV & upto);
                         }
                         cut += csum;
                         nb += __popcll(ENT) - __popcll(LEV);
-                        rem -= __popcll(VAL & lane_range(f, fl + 1));
+                        rem -= __popcll(VALc & lane_range(f, fl + 1));
                         last_flip = rl32(v, fl);
                         compiler_fence();
                         FC_PROF(7, nA_);
