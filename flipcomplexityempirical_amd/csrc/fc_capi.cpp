@@ -72,6 +72,8 @@ struct fc_run {
     bool deal_timed = false;    // d_ctime holds a launch's per-chain durations
     int64_t n_flip_launches = 0;
     int32_t *d_eu = nullptr, *d_ev = nullptr;  // recom: canonical edge list
+    uint32_t *d_nbe = nullptr, *d_eslot = nullptr;  // recom: neighbour rows, edge ends' row indices
+    int32_t nb_d = 4;                          // recom: nbe row length
     uint64_t *d_recom_thresh = nullptr;        // recom: [2E+1] acceptance thresholds
     int8_t *d_ser_a0 = nullptr;  // FC_DIAG_SERIES: assignment at the series window start
     double *d_fs_out = nullptr;  // fc_run_frame_series output (slope, angle), grown on demand
@@ -134,7 +136,7 @@ void free_run(fc_run *r) {
     if (!r) return;
     void *bufs[] = {r->d_graph, r->d_ring_eid, r->d_assign, r->d_fcnt, r->d_sc, r->d_thresh, r->d_log1mp,
                     r->d_labels, r->d_cut_hist, r->d_nb_hist, r->d_edge_acc,
-                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_nfh, r->d_sbits, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_recom_thresh, r->d_tl, r->d_tl_len, r->d_tl_t0,
+                    r->d_num_flips, r->d_part_sum, r->d_last_flipped, r->d_flip_count, r->d_occ_acc, r->d_last_accept, r->d_trace, r->d_tape, r->d_popk, r->d_nfh, r->d_sbits, r->d_mcnt, r->d_ngk, r->d_events, r->d_prof, r->d_eta, r->d_deal, r->d_order, r->d_ctime, r->d_ser_a0, r->d_eu, r->d_ev, r->d_nbe, r->d_eslot, r->d_recom_thresh, r->d_tl, r->d_tl_len, r->d_tl_t0,
                     r->d_fs_out, r->d_fs_cnt, r->d_fc_fuv, r->d_fc_tidx, r->d_fc_tog, r->d_fc_mid, r->d_fc_len,
                     r->d_fc_t0, r->d_fc_cnt, r->d_fc_off, r->d_fc_t, r->d_fc_sa, r->d_fc_wcnt, r->d_st_t, r->d_st_sa};
     for (void *b : bufs)
@@ -782,6 +784,28 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
             HIP_TRY(hipMemcpy(r->d_eu, g.eu.data(), (size_t)E * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(r->d_ev, g.ev.data(), (size_t)E * 4, hipMemcpyHostToDevice));
         }
+        // the neighbours of each node in ring order with their edge ids (node ids and edge ids
+        // < 65535: n <= 8000, degree <= 16), and each edge end's index in the other end's row:
+        // the spanning-tree scan reads one row per node instead of its ring and ring edge ids
+        {
+            const int R = g.ring_max;
+            r->nb_d = std::max(4, (g.max_degree + 3) / 4 * 4);
+            std::vector<uint32_t> nbe((size_t)n * r->nb_d, ~0u), es((size_t)std::max(E, 1), 0u);
+            for (int32_t x = 0; x < n; ++x) {
+                int k = 0;
+                for (int j = 0; j < R; ++j) {
+                    const int32_t e = g.ring_eid[(size_t)x * R + j];
+                    if (e < 0) continue;
+                    nbe[(size_t)x * r->nb_d + k] = (uint32_t)g.ring[(size_t)x * R + j] | ((uint32_t)e << 16);
+                    es[e] |= (uint32_t)k << (g.eu[e] == x ? 0 : 8);
+                    ++k;
+                }
+            }
+            if ((rc = dalloc(&r->d_nbe, nbe.size()))) return rc;
+            if ((rc = dalloc(&r->d_eslot, es.size()))) return rc;
+            HIP_TRY(hipMemcpy(r->d_nbe, nbe.data(), nbe.size() * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(r->d_eslot, es.data(), es.size() * 4, hipMemcpyHostToDevice));
+        }
         // cut_accept: random() < base ** (cut - cut'), cut - cut' in [-E, E]
         const double rb = bases ? bases[0] : p->base;
         std::vector<uint64_t> th(2 * (size_t)E + 1);
@@ -838,6 +862,22 @@ int fc_run_set_initial_wait(fc_run *r, const uint32_t *words) {
     HIP_TRY(hipMemcpy(r->d_sc, sc.data(), sc.size() * sizeof(sc[0]), hipMemcpyHostToDevice));
     return FC_OK;
 }
+
+#ifdef FC_PHASE_PROF
+// diagnostic build: the launch's per-chain phase cycles appended to $FC_PROF_OUT
+static int dump_prof(fc_run *r, hipStream_t s) {
+    if (const char *path = std::getenv("FC_PROF_OUT")) {
+        std::vector<int64_t> h((size_t)r->n_chains * fc::kProfSlots);
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipMemcpy(h.data(), r->d_prof, h.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE *f = std::fopen(path, "ab")) {
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+        }
+    }
+    return FC_OK;
+}
+#endif
 
 int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream) {
     if (!r) return fail(FC_ERR_ARG, "fc_run_steps: null run");
@@ -952,7 +992,9 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     if (r->p.proposal == FC_PROPOSE_RECOM) {
         fc::RecomParams q{};
         q.graph = r->d_graph;
-        q.ring_eid = r->d_ring_eid;
+        q.nbe = r->d_nbe;
+        q.eslot = r->d_eslot;
+        q.nb_d = r->nb_d;
         q.eu = r->d_eu;
         q.ev = r->d_ev;
         q.n = r->g.n;
@@ -976,9 +1018,13 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
         q.trace = (fc_recom_record *)r->d_trace;
         q.trace_chains = r->p.trace_chains;
         q.trace_cap = r->p.trace_cap;
+        q.prof = k.prof;
         const int e = fc::launch_recom(q, r->g.ring_max, s, r->kname, sizeof r->kname);
         if (e != 0) return fail(FC_ERR_HIP, std::string("recom kernel launch: ") + hipGetErrorString((hipError_t)e));
         HIP_TRY(hipEventRecord(evp.second, s));
+#ifdef FC_PHASE_PROF
+        if (int rc = dump_prof(r, s)) return rc;
+#endif
         r->ev0 = evp.first;
         r->ev1 = evp.second;
         r->timed = true;
@@ -1071,15 +1117,7 @@ int fc_run_steps(fc_run *r, int64_t n_steps, int64_t max_draws, void *hip_stream
     }
     HIP_TRY(hipEventRecord(evp.second, s));
 #ifdef FC_PHASE_PROF
-    if (const char *path = std::getenv("FC_PROF_OUT")) {
-        std::vector<int64_t> h((size_t)r->n_chains * fc::kProfSlots);
-        HIP_TRY(hipStreamSynchronize(s));
-        HIP_TRY(hipMemcpy(h.data(), r->d_prof, h.size() * 8, hipMemcpyDeviceToHost));
-        if (FILE *f = std::fopen(path, "ab")) {
-            std::fwrite(h.data(), 8, h.size(), f);
-            std::fclose(f);
-        }
-    }
+    if (int rc = dump_prof(r, s)) return rc;
 #endif
     r->ev0 = evp.first;
     r->ev1 = evp.second;

@@ -191,8 +191,10 @@ constexpr int kNfh = 32;
 // ReCom kernel parameters (fc_recom.hip).
 struct RecomParams {
     const void *graph;             // NodeRec<RMAX>[n]
-    const int32_t *ring_eid;       // [n * RMAX] canonical edge id of each ring neighbour slot
+    const uint32_t *nbe;           // [n * nb_d] neighbours, ring order: id | edge id << 16 (pad ~0u)
+    const uint32_t *eslot;         // [n_edges] k_u | k_v << 8: each end's index in the other's nbe row
     const int32_t *eu, *ev;        // [n_edges] canonical edge list
+    int32_t nb_d;                  // nbe row length: max degree rounded up to a multiple of 4
     int32_t n, n_edges, n_chains, chain_lds_bytes;
     uint32_t chain_id_offset, seed_lo, seed_hi;
     int32_t pop_lo, pop_hi;
@@ -205,6 +207,7 @@ struct RecomParams {
     fc_recom_record *trace;
     int32_t trace_chains;
     int64_t trace_cap;
+    int64_t *prof;                 // [n_chains * kProfSlots] phase cycles (FC_PHASE_PROF builds only)
 };
 inline int recom_lds_bytes(int n) { return 19 * ((n + 15) & ~15) + 16; }
 int launch_recom(const RecomParams &p, int ring_max, void *stream, char *name, size_t name_cap);

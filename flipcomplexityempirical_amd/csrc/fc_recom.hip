@@ -41,6 +41,8 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 
 __device__ __forceinline__ uint64_t mulhi64(uint64_t r, uint64_t n) { return __umul64hi(r, n); }
 
+__device__ __forceinline__ uint32_t word4(const uint4 &w, int t) { return t == 0 ? w.x : t == 1 ? w.y : t == 2 ? w.z : w.w; }
+
 __device__ __forceinline__ int64_t wave_sum64(int64_t x) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor((long long)x, off);
@@ -71,6 +73,15 @@ __device__ int kth_item(int count, int lane, uint64_t k, F flag, int &total) {
     return own ? __builtin_amdgcn_readlane(found, __builtin_ctzll(own)) : -1;
 }
 
+#ifndef FC_RECOM_SCAN_U
+#define FC_RECOM_SCAN_U 2
+#endif
+#ifndef FC_RECOM_JUMP_U
+#define FC_RECOM_JUMP_U 4
+#endif
+constexpr int kScanU8 = FC_RECOM_SCAN_U;  // Boruvka scan: nodes per lane in flight (RMAX = 8; 2 for 16)
+constexpr int kJumpU = FC_RECOM_JUMP_U;  // pointer jumping: nodes per lane in flight
+
 template <int RMAX>
 __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -83,13 +94,15 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
     unsigned char *base = smem + (size_t)wv * p.chain_lds_bytes;
     uint64_t *best = (uint64_t *)base;                    // [npad] Boruvka best key; then int32 spop
     int32_t *spop = (int32_t *)best;
-    uint32_t *tadj = (uint32_t *)(best + npad);          // [npad] tree slots (bits 0-15), subset mark (31)
+    uint32_t *tadj = (uint32_t *)(best + npad);          // [npad] tree edges (bit k: row entry k), subset mark (31)
     int16_t *comp = (int16_t *)(tadj + npad);            // [npad] component; then level starts
     int16_t *order = comp + npad;                        // [npad] hook targets; then BFS order
     int16_t *par = order + npad;                         // [npad]
     int8_t *a = (int8_t *)(par + npad);                  // [npad]
-    int32_t *cnt = (int32_t *)(a + npad);                // [4] counters
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
+    constexpr int kScanU = RMAX == 8 ? kScanU8 : 2;
+    const uint4 *__restrict__ NB = (const uint4 *)p.nbe;  // neighbour rows, nq vectors each
+    const int nq = p.nb_d >> 2;
 
     {
         const uint4 *ga = (const uint4 *)(p.assign + (size_t)c * npad);
@@ -107,7 +120,16 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
     const uint32_t gid = p.chain_id_offset + (uint32_t)c;
     const bool trace_on = p.trace && c < p.trace_chains;
     int64_t rem = p.n_steps;
+#ifdef FC_PHASE_PROF
+    // phase cycles (diagnostic build; tools/prof_recom_report.py): 0 loop, 1 edge + popM,
+    // 2 spanning trees, 3 Boruvka scans, 4 hooks, 5 pointer jumps, 6 root choice, 7 BFS order,
+    // 8 subtree sums, 9 cut choice, 10 subset marks, 11 step 5; counts: 12 Boruvka rounds,
+    // 13 BFS levels, 14 trees, 15 pointer-jump passes, 16 proposals, 17 attempts
+    int64_t *prof_acc = (int64_t *)(base + p.chain_lds_bytes - kProfSlots * 8);
+    if (lane < kProfSlots) prof_acc[lane] = 0;
+#endif
     wave_sync();
+    FC_STAMP(t_loop0);
 
     while (rem > 0) {
         if (draw >= draw_cap) {
@@ -115,6 +137,8 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
             break;
         }
         const uint64_t d = draw++;
+        FC_STAMP(t_s0);
+        FC_PROF(16, 1);
         const Words4 w = philox4x32_10((uint32_t)d, (uint32_t)(d >> 32), gid, 0u, p.seed_lo, p.seed_hi);
         // ---- 1. recom: edge = random.choice(tuple(partition["cut_edges"])) ----------------
         int tot = 0;
@@ -126,13 +150,18 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
         for (int x = lane; x < n; x += kWave) pm += inM(x) ? G[x].pop : 0;
         const int64_t popM = wave_sum64(pm);
         ++proposals;
+        FC_STAMP(t_s1);
+        FC_PROF(1, t_s1 - t_s0);
         // ---- 2-4. bipartition_tree ----------------------------------------------------
         int tree = -1, root = -1, child = -1, attempts = 0;
         for (int t = 0; t < p.max_attempts; ++t) {
             ++attempts;
+            FC_PROF(17, 1);
             if (t / p.node_repeats != tree) {
                 tree = t / p.node_repeats;
                 ++trees_tot;
+                FC_STAMP(t_tr0);
+                FC_PROF(14, 1);
                 const Words4 kw = philox4x32_10((uint32_t)d, (uint32_t)(d >> 32), gid, 0x80000000u | (uint32_t)tree,
                                                 p.seed_lo, p.seed_hi);
                 const uint64_t key = ((uint64_t)kw.x1 << 32) | kw.x0;
@@ -143,80 +172,113 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                 }
                 wave_sync();
                 for (;;) {
+                    FC_STAMP(t_b0);
+                    FC_PROF(12, 1);
                     for (int x = lane; x < n; x += kWave) best[x] = 0;
                     wave_sync();
-                    for (int x = lane; x < n; x += kWave) {
-                        const int cx = comp[x];
-                        if (cx < 0) continue;
-                        const NodeRec<RMAX> r = G[x];
-                        // the node's ring edge ids (static, RMAX / 4 vector loads) and its ring
-                        // cells' components, every read issued before the first use (one at a time
-                        // behind each neighbour test before: a dependent L2 and LDS round trip per
-                        // edge); the keys are then formed by selects, without a branch per cell
-                        int4 er[RMAX / 4];
-                        const int4 *rp = (const int4 *)(p.ring_eid + (size_t)x * RMAX);
+                    // kScanU nodes per lane at a time: their neighbour rows (nb_d / 4 vector
+                    // loads: ids and edge ids) and the neighbours' components, every read issued
+                    // before the first use; the keys are then formed by selects, without a branch
+                    // per neighbour (a row holds the neighbours only: a ring's other cells cost
+                    // no weight)
+                    for (int x0 = lane; x0 < n; x0 += kScanU * kWave) {
+                        int cxs[kScanU];
+                        uint4 nw[kScanU][RMAX / 4];
 #pragma unroll
-                        for (int q = 0; q < RMAX / 4; ++q) er[q] = rp[q];
-                        const uint32_t nbr = (uint32_t)(r.meta >> kMetaNbrShift) & 0xffffu;
-                        int cyv[RMAX];
+                        for (int u = 0; u < kScanU; ++u) {
+                            const int x = x0 + u * kWave;
+                            cxs[u] = x < n ? (int)comp[x] : -1;
+                            const int xc = x < n ? x : x0;
 #pragma unroll
-                        for (int j = 0; j < RMAX; ++j) cyv[j] = comp[ring_entry<RMAX>(r.ring, j)];
-#pragma unroll
-                        for (int j = 0; j < RMAX; ++j) asm volatile("" : "+v"(cyv[j]));
-                        uint64_t bk = 0;
-#pragma unroll
-                        for (int j = 0; j < RMAX; ++j) {
-                            const int4 eq = er[j >> 2];
-                            const int ej = (j & 3) == 0 ? eq.x : (j & 3) == 1 ? eq.y : (j & 3) == 2 ? eq.z : eq.w;
-                            const bool use = ((nbr >> j) & 1u) && cyv[j] >= 0 && cyv[j] != cx;
-                            const uint32_t e = (uint32_t)ej;
-                            const uint64_t kk = ((splitmix64(key + (uint64_t)e) >> 32) << 32) | (0xffffffffu - e);
-                            bk = (use && kk > bk) ? kk : bk;
+                            for (int q = 0; q < RMAX / 4; ++q)
+                                nw[u][q] = q < nq ? NB[(size_t)xc * nq + q] : make_uint4(~0u, ~0u, ~0u, ~0u);
                         }
-                        if (bk) atomicMax((unsigned long long *)&best[cx], (unsigned long long)bk);
+                        int cyv[kScanU][RMAX];
+#pragma unroll
+                        for (int u = 0; u < kScanU; ++u)
+#pragma unroll
+                            for (int j = 0; j < RMAX; ++j) {
+                                const uint32_t nb = word4(nw[u][j >> 2], j & 3) & 0xffffu;
+                                cyv[u][j] = nb != 0xffffu ? (int)comp[nb] : -1;
+                            }
+#pragma unroll
+                        for (int u = 0; u < kScanU; ++u)
+#pragma unroll
+                            for (int j = 0; j < RMAX; ++j) asm volatile("" : "+v"(cyv[u][j]));
+#pragma unroll
+                        for (int u = 0; u < kScanU; ++u) {
+                            const int cx = cxs[u];
+                            uint64_t bk = 0;
+#pragma unroll
+                            for (int q = 0; q < RMAX / 4; ++q) {
+                                if (q >= nq) break;
+#pragma unroll
+                                for (int t4 = 0; t4 < 4; ++t4) {
+                                    const int j = 4 * q + t4;
+                                    const uint32_t e = word4(nw[u][q], t4) >> 16;
+                                    const bool use = cx >= 0 && cyv[u][j] >= 0 && cyv[u][j] != cx;
+                                    const uint64_t kk = ((splitmix64(key + (uint64_t)e) >> 32) << 32) | (0xffffffffu - e);
+                                    bk = (use && kk > bk) ? kk : bk;
+                                }
+                            }
+                            if (bk) atomicMax((unsigned long long *)&best[cx], (unsigned long long)bk);
+                        }
                     }
                     wave_sync();
+                    FC_STAMP(t_b1);
+                    FC_PROF(3, t_b1 - t_b0);
                     bool hooked = false;
                     for (int x = lane; x < n; x += kWave) {
-                        if (comp[x] != x || best[x] == 0) continue;
+                        if (comp[x] != x) continue;
                         const uint64_t bx = best[x];
+                        if (bx == 0) {  // no edge out (M's last component)
+                            order[x] = (int16_t)x;
+                            continue;
+                        }
                         const int e = (int)(0xffffffffu - (uint32_t)bx);
                         const int u = p.eu[e], v = p.ev[e];
+                        const uint32_t ks = p.eslot[e];
                         const int other = comp[u] == x ? comp[v] : comp[u];
                         order[x] = (best[other] == bx && x < other) ? (int16_t)x : (int16_t)other;  // hook
                         hooked = true;
-                        // record the tree edge on both endpoints (ring slot of the other end)
-                        const NodeRec<RMAX> ru = G[u], rv = G[v];
-                        uint32_t su = 0, sv = 0;
-#pragma unroll
-                        for (int j = 0; j < RMAX; ++j) {
-                            su |= (uint32_t)(ring_entry<RMAX>(ru.ring, j) == v && ((ru.meta >> (kMetaNbrShift + j)) & 1u)) << j;
-                            sv |= (uint32_t)(ring_entry<RMAX>(rv.ring, j) == u && ((rv.meta >> (kMetaNbrShift + j)) & 1u)) << j;
-                        }
-                        atomicOr(&tadj[u], su);
-                        atomicOr(&tadj[v], sv);
+                        // record the tree edge on both endpoints (the other end's index in the row)
+                        atomicOr(&tadj[u], 1u << (ks & 0xffu));
+                        atomicOr(&tadj[v], 1u << (ks >> 8));
                     }
                     wave_sync();
+                    FC_STAMP(t_b2);
+                    FC_PROF(4, t_b2 - t_b1);
                     if (!__any(hooked)) break;
-                    for (int x = lane; x < n; x += kWave)
-                        if (comp[x] == x && best[x] != 0) comp[x] = order[x];
-                    wave_sync();
-                    for (;;) {  // pointer jumping to the new roots
-                        bool ch = false;
-                        for (int x = lane; x < n; x += kWave) {
-                            const int cx = comp[x];
-                            if (cx < 0) continue;
-                            const int cc = comp[cx];
-                            if (cc != cx) {
-                                comp[x] = (int16_t)cc;
-                                ch = true;
-                            }
-                        }
-                        wave_sync();
-                        if (!__any(ch)) break;
+                    // the new roots: every old root follows its hook targets to the one hooked onto
+                    // itself (distinct keys: the only cycles are mutual hooks, broken by id), then
+                    // every node takes its old root's new root -- two passes, where pointer jumping
+                    // over all nodes took about four per round
+                    FC_PROF(15, 1);
+                    for (int x = lane; x < n; x += kWave) {
+                        if (comp[x] != x) continue;
+                        int r = order[x];
+                        for (int r2 = order[r]; r2 != r; r2 = order[r]) r = r2;
+                        order[x] = (int16_t)r;
                     }
+                    wave_sync();
+                    for (int x0 = lane; x0 < n; x0 += kJumpU * kWave) {  // kJumpU reads in flight
+                        int cxs[kJumpU], rts[kJumpU];
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u) cxs[u] = x0 + u * kWave < n ? (int)comp[x0 + u * kWave] : -1;
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u) rts[u] = cxs[u] >= 0 ? (int)order[cxs[u]] : -1;
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u)
+                            if (rts[u] != cxs[u]) comp[x0 + u * kWave] = (int16_t)rts[u];
+                    }
+                    wave_sync();
+                    FC_STAMP(t_b3);
+                    FC_PROF(5, t_b3 - t_b2);
                 }
+                FC_STAMP(t_tr1);
+                FC_PROF(2, t_tr1 - t_tr0);
             }
+            FC_STAMP(t_r0);
             const Words4 cw = philox4x32_10((uint32_t)d, (uint32_t)(d >> 32), gid, 0x40000000u | (uint32_t)t,
                                             p.seed_lo, p.seed_hi);
             // root = choice([x for x in h if h.degree(x) > 1]), ascending node id
@@ -233,38 +295,98 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
             }
             if (nr_tot == 0) continue;
             root = kth_item(n, lane, mulhi64(((uint64_t)cw.x1 << 32) | cw.x0, (uint64_t)nr_tot), is_inner, nroot);
-            // BFS order over the tree; level starts in comp[]
+            FC_STAMP(t_r1);
+            FC_PROF(6, t_r1 - t_r0);
+            // the tree's adjacency as a CSR in the Boruvka keys' space (dead until the subtree sums):
+            // offsets by a wave scan of the tree degrees, neighbour ids from the ring slots
+            int16_t *toff = (int16_t *)best;       // [n + 1]
+            int16_t *tnb = toff + ((n + 2) & ~1);  // [2 (|M| - 1)]
+            {
+                int ob = 0;
+                for (int x0 = 0; x0 < n; x0 += kWave) {
+                    const int x = x0 + lane;
+                    const int dg = x < n ? __popc(tadj[x] & 0xffffu) : 0;
+                    const int incl = wave_scan_incl(dg);
+                    if (x < n) toff[x] = (int16_t)(ob + incl - dg);
+                    ob += __builtin_amdgcn_readlane(incl, kWave - 1);
+                }
+                if (lane == 0) toff[n] = (int16_t)ob;
+                for (int x0 = lane; x0 < n; x0 += kScanU * kWave) {
+                    uint32_t tbs[kScanU];
+                    int os[kScanU];
+                    uint4 nw[kScanU][RMAX / 4];
+#pragma unroll
+                    for (int u = 0; u < kScanU; ++u) {
+                        const int x = x0 + u * kWave;
+                        const int xc = x < n ? x : x0;
+                        tbs[u] = x < n ? (tadj[x] & 0xffffu) : 0u;
+                        os[u] = toff[xc];
+#pragma unroll
+                        for (int q = 0; q < RMAX / 4; ++q)
+                            nw[u][q] = q < nq ? NB[(size_t)xc * nq + q] : make_uint4(~0u, ~0u, ~0u, ~0u);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kScanU; ++u) {
+                        int o = os[u];
+#pragma unroll
+                        for (int j = 0; j < RMAX; ++j)
+                            if ((tbs[u] >> j) & 1u) tnb[o++] = (int16_t)(word4(nw[u][j >> 2], j & 3) & 0xffffu);
+                    }
+                }
+            }
+            wave_sync();
+            // BFS order over the tree, a level at a time; children placed by a wave scan of the
+            // child counts; level starts in comp[]
             if (lane == 0) {
                 order[0] = (int16_t)root;
                 par[root] = -1;
-                cnt[0] = 1;
                 comp[0] = 0;
                 comp[1] = 1;
             }
             wave_sync();
             int L = 0;
-            for (;;) {
-                const int ls = comp[L], le = comp[L + 1];
-                if (ls == le) break;
-                for (int i = ls + lane; i < le; i += kWave) {
-                    const int x = order[i];
-                    const NodeRec<RMAX> r = G[x];
-                    const uint32_t tb = tadj[x] & 0xffffu;
+            {
+                int ls = 0, le = 1;
+                while (ls < le) {
+                    int nb_end = le;
+                    for (int i0 = ls; i0 < le; i0 += kWave) {
+                        const int i = i0 + lane;
+                        int x = 0, o0 = 0, o1 = 0, px = -1;
+                        if (i < le) {
+                            x = order[i];
+                            o0 = toff[x];
+                            o1 = toff[x + 1];
+                            px = par[x];
+                        }
+                        const int nch = o1 - o0 - (px >= 0 ? 1 : 0);
+                        const int incl = wave_scan_incl(nch);
+                        int pos = nb_end + incl - nch;
+                        nb_end += __builtin_amdgcn_readlane(incl, kWave - 1);
+                        // every child read issued at once (entries past o1 stay inside the keys'
+                        // space: tnb has room for 4 npad - n - 2 >= 2 n + RMAX of them)
+                        int yv[RMAX];
 #pragma unroll
-                    for (int j = 0; j < RMAX; ++j) {
-                        if (!((tb >> j) & 1u)) continue;
-                        const int y = ring_entry<RMAX>(r.ring, j);
-                        if (y == par[x]) continue;
-                        const int pos = atomicAdd(&cnt[0], 1);
-                        order[pos] = (int16_t)y;
-                        par[y] = (int16_t)x;
+                        for (int j = 0; j < RMAX; ++j) yv[j] = tnb[o0 + j];
+#pragma unroll
+                        for (int j = 0; j < RMAX; ++j) asm volatile("" : "+v"(yv[j]));
+#pragma unroll
+                        for (int j = 0; j < RMAX; ++j) {
+                            if (o0 + j >= o1 || yv[j] == px) continue;
+                            order[pos++] = (int16_t)yv[j];
+                            par[yv[j]] = (int16_t)x;
+                        }
                     }
+                    wave_sync();
+                    ++L;
+                    ls = le;
+                    le = nb_end;
+                    if (lane == 0) comp[L + 1] = (int16_t)le;
                 }
-                wave_sync();
-                ++L;
-                if (lane == 0) comp[L + 1] = (int16_t)cnt[0];
-                wave_sync();
             }
+            wave_sync();
+            FC_STAMP(t_r2);
+            FC_PROF(7, t_r2 - t_r1);
+            FC_PROF(13, L);
             // subtree populations, leaves upward
             const int nM = comp[L];
             for (int i = lane; i < nM; i += kWave) {
@@ -279,6 +401,8 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                 }
                 wave_sync();
             }
+            FC_STAMP(t_r3);
+            FC_PROF(8, t_r3 - t_r2);
             // cuts: |pop(subtree(x)) - ideal| < epsilon * ideal (has_ideal_population)
             auto is_cut = [&](int x) {
                 return inM(x) && x != root && fabs((double)spop[x] - p.pop_target) < p.epsilon * p.pop_target;
@@ -294,6 +418,8 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
             if (ncut == 0) continue;
             int dummy = 0;
             child = kth_item(n, lane, mulhi64(((uint64_t)cw.x3 << 32) | cw.x2, (uint64_t)ncut), is_cut, dummy);
+            FC_STAMP(t_r4);
+            FC_PROF(9, t_r4 - t_r3);
             // subset = subtree(child): marks flow down the BFS levels
             if (lane == 0) atomicOr(&tadj[child], 0x80000000u);
             wave_sync();
@@ -304,6 +430,8 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                 }
                 wave_sync();
             }
+            FC_STAMP(t_r5);
+            FC_PROF(10, t_r5 - t_r4);
             break;
         }
         attempts_tot += attempts;
@@ -312,6 +440,7 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
             break;
         }
         // ---- 5. the proposed state: subtree(child) -> parts[0], rest of M -> parts[1] --------
+        FC_STAMP(t_5a);
         auto na = [&](int x) -> int { return inM(x) ? ((tadj[x] & 0x80000000u) ? d0 : d1) : a[x]; };
         int cc = 0;
         for (int e = lane; e < E; e += kWave) cc += na(p.eu[e]) != na(p.ev[e]);
@@ -362,7 +491,16 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
         if (trace_on) ++trace_len;
         for (int x = lane; x < npad; x += kWave) tadj[x] &= 0x7fffffffu;
         wave_sync();
+        FC_STAMP(t_5b);
+        FC_PROF(11, t_5b - t_5a);
     }
+    FC_STAMP(t_loop1);
+    FC_PROF(0, t_loop1 - t_loop0);
+#ifdef FC_PHASE_PROF
+    wave_sync();
+    if (lane == 0)
+        for (int i = 0; i < kProfSlots; ++i) p.prof[(size_t)c * kProfSlots + i] = prof_acc[i];
+#endif
 
     // ---- write back ---------------------------------------------------------------------
     {

@@ -23,17 +23,25 @@ CASES = {
     "sec11 k=2": ("sec11", 2, "sec11:0", 0.1, 0.05, 1, 1.0, 60),
     "sec11 k=4 cut_accept": ("sec11", 4, "quadrant", 0.1, 0.05, 1, 1.5, 80),
     "frank k=2 node_repeats=2": ("frank", 2, "frank:1", 0.1, 0.05, 2, 1.0, 60),
+    # neighbour rows of two vectors (degree 6) and the RMAX = 16 instance (Delaunay dual)
+    "triangular k=3": ("tri", 3, "strip", 0.2, 0.1, 1, 1.0, 40),
+    "delaunay k=2": ("delaunay", 2, "bisect", 0.2, 0.1, 1, 1.0, 30),
 }
 
 
 def _setup(case):
     gname, k, plan, pct, eps, reps, base, steps = CASES[case]
-    spec = G.sec11_graph() if gname == "sec11" else G.frank_graph()
-    labels = [-1, 1] if k == 2 else list(range(k))
+    spec = {"sec11": G.sec11_graph, "frank": G.frank_graph, "tri": lambda: G.triangular_graph(20, 38),
+            "delaunay": lambda: G.delaunay_graph(1500, seed=3)}[gname]()
+    labels = [-1, 1] if k == 2 and plan.startswith(("sec11", "frank")) else list(range(k))
     if plan.startswith("sec11"):
         a0 = spec.assignment_array(G.sec11_plan(int(plan[-1]), spec.nodes), labels)
     elif plan.startswith("frank"):
         a0 = spec.assignment_array(G.frank_plan(int(plan[-1]), spec.nodes), labels)
+    elif plan == "strip":
+        a0 = spec.assignment_array(G.strip_plan(spec, k), labels)
+    elif plan == "bisect":
+        a0 = spec.assignment_array(G.bisection_plan(spec, k), labels)
     else:
         a0 = spec.assignment_array(G.quadrant_plan(spec.nodes), labels)
     total = int(spec.pop.sum())
@@ -52,7 +60,7 @@ def test_recom_matches_oracle(gpu, case):
     run.steps(steps // 2)
     run.steps(steps - steps // 2)  # across launches
     st, fin = run.stats(), run.state()
-    assert run.kernel_name().startswith("fc::recom_kernel<")
+    assert run.kernel_name() == ("fc::recom_kernel<16>" if case.startswith("delaunay") else "fc::recom_kernel<8>")
     for c in range(n_chains):
         ref = recom_run(spec, a0, k=k, pop_target=ideal, epsilon=eps, pop_lo=lo, pop_hi=hi, seed=99, chain_id=c,
                         n_steps=steps, node_repeats=reps, base=base, trace_cap=4 * steps)
