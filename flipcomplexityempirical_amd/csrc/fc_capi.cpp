@@ -426,8 +426,9 @@ int fc_run_create(const fc_graph *gr, const fc_params *p, int32_t n_chains, cons
     r->words = (n + 63) / 64;
     if (g.max_degree > 16)  // dev::wave_bfs labels each old neighbour with a 4-bit id
         return fail(FC_ERR_UNSUPPORTED, "fc_run_create: node degree above 16");
-    if (recom)   // fc_recom.hip: best / spop, tree slots, component / levels, order, parent, a
-        r->chain_lds_bytes = fc::recom_lds_bytes(n);
+    if (recom)   // fc_recom.hip: keys / tree CSR + parents / subtree populations, component /
+                 // levels, order, tree-edge bits, a
+        r->chain_lds_bytes = fc::recom_lds_bytes(n, g.ring_max);
     else if (k == 2)  // fc_flip2.hip: a, fcnt, thresholds, 3 BFS bitmaps, slots, commit marks (2 npad + 16),
                       // wait / tally queue (24 B per entry), launch start time, pace, first queued yield,
                       // tally-log length, launch's first yield (40) (sec11: 10,032 B, so 16 chains still

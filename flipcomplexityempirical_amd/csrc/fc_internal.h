@@ -209,7 +209,9 @@ struct RecomParams {
     int64_t trace_cap;
     int64_t *prof;                 // [n_chains * kProfSlots] phase cycles (FC_PHASE_PROF builds only)
 };
-inline int recom_lds_bytes(int n) { return 19 * ((n + 15) & ~15) + 16; }
+// fc_recom.hip's layout: 8 B (keys / tree CSR + parents / subtree populations) + component +
+// order (2 + 2 B) + tree-edge bits (1 B for RMAX = 8, else 2) + assignment (1 B) per node
+inline int recom_lds_bytes(int n, int ring_max) { return (ring_max == 8 ? 14 : 15) * ((n + 15) & ~15); }
 int launch_recom(const RecomParams &p, int ring_max, void *stream, char *name, size_t name_cap);
 
 // Launch wrappers (fc_kernels.hip).  Return a hipError_t as int.

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <type_traits>
 
 #include "fc_device.h"
 #include "fc_internal.h"
@@ -92,13 +93,27 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
     const int n = p.n, E = p.n_edges;
     const int npad = (n + 15) & ~15;
     unsigned char *base = smem + (size_t)wv * p.chain_lds_bytes;
-    uint64_t *best = (uint64_t *)base;                    // [npad] Boruvka best key; then int32 spop
+    // LDS layout (recom_lds_bytes: 14 B per node for RMAX = 8, 15 for 16; the kernel is
+    // latency-bound, so the chains a CU holds set its rate):
+    //   [0, 8 npad)   Boruvka keys; then the tree's CSR [0, 6 npad) and the BFS parents
+    //                 [6 npad, 8 npad); then subtree populations [0, 4 npad) (sign bit: subset mark)
+    //   comp          component; then level starts
+    //   order         hook targets; then BFS order
+    //   tadj          tree edges (bit k: neighbour row entry k)
+    //   a             assignment
+    using TAdj = typename std::conditional<RMAX == 8, uint8_t, uint16_t>::type;
+    uint64_t *best = (uint64_t *)base;
     int32_t *spop = (int32_t *)best;
-    uint32_t *tadj = (uint32_t *)(best + npad);          // [npad] tree edges (bit k: row entry k), subset mark (31)
-    int16_t *comp = (int16_t *)(tadj + npad);            // [npad] component; then level starts
-    int16_t *order = comp + npad;                        // [npad] hook targets; then BFS order
-    int16_t *par = order + npad;                         // [npad]
-    int8_t *a = (int8_t *)(par + npad);                  // [npad]
+    int16_t *par = (int16_t *)(base + 6 * (size_t)npad);
+    int16_t *comp = (int16_t *)(best + npad);
+    int16_t *order = comp + npad;
+    TAdj *tadj = (TAdj *)(order + npad);
+    int8_t *a = (int8_t *)(tadj + npad);
+    // tree-edge bits by 32-bit LDS atomics on the word holding the node's entry
+    auto tadj_or = [&](int x, uint32_t bits) {
+        constexpr int kPer = 4 / (int)sizeof(TAdj);
+        atomicOr((uint32_t *)tadj + x / kPer, bits << (8 * (int)sizeof(TAdj) * (x % kPer)));
+    };
     const NodeRec<RMAX> *__restrict__ G = (const NodeRec<RMAX> *)p.graph;
     constexpr int kScanU = RMAX == 8 ? kScanU8 : 2;
     const uint4 *__restrict__ NB = (const uint4 *)p.nbe;  // neighbour rows, nq vectors each
@@ -154,6 +169,7 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
         FC_PROF(1, t_s1 - t_s0);
         // ---- 2-4. bipartition_tree ----------------------------------------------------
         int tree = -1, root = -1, child = -1, attempts = 0;
+        int64_t p0 = 0;  // subtree(child)'s population
         for (int t = 0; t < p.max_attempts; ++t) {
             ++attempts;
             FC_PROF(17, 1);
@@ -242,8 +258,8 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                         order[x] = (best[other] == bx && x < other) ? (int16_t)x : (int16_t)other;  // hook
                         hooked = true;
                         // record the tree edge on both endpoints (the other end's index in the row)
-                        atomicOr(&tadj[u], 1u << (ks & 0xffu));
-                        atomicOr(&tadj[v], 1u << (ks >> 8));
+                        tadj_or(u, 1u << (ks & 0xffu));
+                        tadj_or(v, 1u << (ks >> 8));
                     }
                     wave_sync();
                     FC_STAMP(t_b2);
@@ -283,7 +299,7 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                                             p.seed_lo, p.seed_hi);
             // root = choice([x for x in h if h.degree(x) > 1]), ascending node id
             int nroot = 0;
-            auto is_inner = [&](int x) { return inM(x) && __popc(tadj[x] & 0xffffu) > 1; };
+            auto is_inner = [&](int x) { return inM(x) && __popc((uint32_t)tadj[x]) > 1; };
             int nr_tot = 0;
             {
                 // count first (the choice multiplies by the count)
@@ -305,7 +321,7 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                 int ob = 0;
                 for (int x0 = 0; x0 < n; x0 += kWave) {
                     const int x = x0 + lane;
-                    const int dg = x < n ? __popc(tadj[x] & 0xffffu) : 0;
+                    const int dg = x < n ? __popc((uint32_t)tadj[x]) : 0;
                     const int incl = wave_scan_incl(dg);
                     if (x < n) toff[x] = (int16_t)(ob + incl - dg);
                     ob += __builtin_amdgcn_readlane(incl, kWave - 1);
@@ -319,7 +335,7 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                     for (int u = 0; u < kScanU; ++u) {
                         const int x = x0 + u * kWave;
                         const int xc = x < n ? x : x0;
-                        tbs[u] = x < n ? (tadj[x] & 0xffffu) : 0u;
+                        tbs[u] = x < n ? (uint32_t)tadj[x] : 0u;
                         os[u] = toff[xc];
 #pragma unroll
                         for (int q = 0; q < RMAX / 4; ++q)
@@ -421,12 +437,13 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
             FC_STAMP(t_r4);
             FC_PROF(9, t_r4 - t_r3);
             // subset = subtree(child): marks flow down the BFS levels
-            if (lane == 0) atomicOr(&tadj[child], 0x80000000u);
+            p0 = spop[child];
+            if (lane == 0) spop[child] |= (int32_t)0x80000000u;
             wave_sync();
             for (int l = 1; l < L; ++l) {
                 for (int i = comp[l] + lane; i < comp[l + 1]; i += kWave) {
                     const int x = order[i];
-                    if (tadj[par[x]] & 0x80000000u) atomicOr(&tadj[x], 0x80000000u);
+                    if (spop[par[x]] < 0) spop[x] |= (int32_t)0x80000000u;
                 }
                 wave_sync();
             }
@@ -441,11 +458,11 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
         }
         // ---- 5. the proposed state: subtree(child) -> parts[0], rest of M -> parts[1] --------
         FC_STAMP(t_5a);
-        auto na = [&](int x) -> int { return inM(x) ? ((tadj[x] & 0x80000000u) ? d0 : d1) : a[x]; };
+        auto na = [&](int x) -> int { return inM(x) ? (spop[x] < 0 ? d0 : d1) : a[x]; };
         int cc = 0;
         for (int e = lane; e < E; e += kWave) cc += na(p.eu[e]) != na(p.ev[e]);
         const int cut_new = (int)wave_sum64(cc);
-        const int64_t p0 = spop[child], p1 = popM - p0;
+        const int64_t p1 = popM - p0;
         int flags;
         if (p0 < pop_lo || p0 > pop_hi || p1 < pop_lo || p1 > pop_hi) {
             ++inv_pop;
@@ -489,7 +506,6 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
             rr.cut = cut;
         }
         if (trace_on) ++trace_len;
-        for (int x = lane; x < npad; x += kWave) tadj[x] &= 0x7fffffffu;
         wave_sync();
         FC_STAMP(t_5b);
         FC_PROF(11, t_5b - t_5a);
