@@ -181,10 +181,24 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                 const Words4 kw = philox4x32_10((uint32_t)d, (uint32_t)(d >> 32), gid, 0x80000000u | (uint32_t)tree,
                                                 p.seed_lo, p.seed_hi);
                 const uint64_t key = ((uint64_t)kw.x1 << 32) | kw.x0;
-                // Boruvka maximum spanning tree of M (weights with edge-id tie break)
-                for (int x = lane; x < npad; x += kWave) {
-                    comp[x] = (x < n && inM(x)) ? (int16_t)x : (int16_t)-1;
-                    tadj[x] = 0;
+                // Boruvka maximum spanning tree of M (weights with edge-id tie break).  A root's
+                // hook target goes to the high half of its key word (the low half, ~edge id, still
+                // tells a mutual hook); order[] holds the active nodes -- those with a neighbour in
+                // another component at the last scan (components only merge, so a node without one
+                // never has one again), kept in node order
+                auto tgt = [&](int x) -> int { return ((const int32_t *)best)[2 * x + 1]; };
+                auto set_tgt = [&](int x, int r) { ((int32_t *)best)[2 * x + 1] = r; };
+                int m_act = 0;
+                for (int x0 = 0; x0 < npad; x0 += kWave) {
+                    const int x = x0 + lane;
+                    const bool in = x < n && inM(x);
+                    if (x < npad) {  // (npad is a multiple of 16 only)
+                        comp[x] = in ? (int16_t)x : (int16_t)-1;
+                        tadj[x] = 0;
+                    }
+                    const int incl = wave_scan_incl(in ? 1 : 0);
+                    if (in) order[m_act + incl - 1] = (int16_t)x;
+                    m_act += __builtin_amdgcn_readlane(incl, kWave - 1);
                 }
                 wave_sync();
                 for (;;) {
@@ -192,19 +206,24 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                     FC_PROF(12, 1);
                     for (int x = lane; x < n; x += kWave) best[x] = 0;
                     wave_sync();
-                    // kScanU nodes per lane at a time: their neighbour rows (nb_d / 4 vector
-                    // loads: ids and edge ids) and the neighbours' components, every read issued
-                    // before the first use; the keys are then formed by selects, without a branch
-                    // per neighbour (a row holds the neighbours only: a ring's other cells cost
-                    // no weight)
-                    for (int x0 = lane; x0 < n; x0 += kScanU * kWave) {
-                        int cxs[kScanU];
+                    // kScanU active nodes per lane at a time: their neighbour rows (nb_d / 4
+                    // vector loads: ids and edge ids) and the neighbours' components, every read
+                    // issued before the first use; the keys are then formed by selects, without a
+                    // branch per neighbour (a row holds the neighbours only: a ring's other cells
+                    // cost no weight); the nodes still active are written back in order
+                    int m_next = 0;
+                    for (int i0 = 0; i0 < m_act; i0 += kScanU * kWave) {
+                        int xs[kScanU], cxs[kScanU];
                         uint4 nw[kScanU][RMAX / 4];
 #pragma unroll
                         for (int u = 0; u < kScanU; ++u) {
-                            const int x = x0 + u * kWave;
-                            cxs[u] = x < n ? (int)comp[x] : -1;
-                            const int xc = x < n ? x : x0;
+                            const int i = i0 + u * kWave + lane;
+                            xs[u] = i < m_act ? (int)order[i] : -1;
+                        }
+#pragma unroll
+                        for (int u = 0; u < kScanU; ++u) {
+                            const int xc = xs[u] >= 0 ? xs[u] : 0;
+                            cxs[u] = xs[u] >= 0 ? (int)comp[xc] : -1;
 #pragma unroll
                             for (int q = 0; q < RMAX / 4; ++q)
                                 nw[u][q] = q < nq ? NB[(size_t)xc * nq + q] : make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -225,6 +244,7 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                         for (int u = 0; u < kScanU; ++u) {
                             const int cx = cxs[u];
                             uint64_t bk = 0;
+                            bool any = false;
 #pragma unroll
                             for (int q = 0; q < RMAX / 4; ++q) {
                                 if (q >= nq) break;
@@ -233,13 +253,19 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                                     const int j = 4 * q + t4;
                                     const uint32_t e = word4(nw[u][q], t4) >> 16;
                                     const bool use = cx >= 0 && cyv[u][j] >= 0 && cyv[u][j] != cx;
+                                    any |= use;
                                     const uint64_t kk = ((splitmix64(key + (uint64_t)e) >> 32) << 32) | (0xffffffffu - e);
                                     bk = (use && kk > bk) ? kk : bk;
                                 }
                             }
                             if (bk) atomicMax((unsigned long long *)&best[cx], (unsigned long long)bk);
+                            // (positions <= the entries this iteration read: in-place is safe)
+                            const int incl = wave_scan_incl(any ? 1 : 0);
+                            if (any) order[m_next + incl - 1] = (int16_t)xs[u];
+                            m_next += __builtin_amdgcn_readlane(incl, kWave - 1);
                         }
                     }
+                    m_act = m_next;
                     wave_sync();
                     FC_STAMP(t_b1);
                     FC_PROF(3, t_b1 - t_b0);
@@ -248,14 +274,15 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                         if (comp[x] != x) continue;
                         const uint64_t bx = best[x];
                         if (bx == 0) {  // no edge out (M's last component)
-                            order[x] = (int16_t)x;
+                            set_tgt(x, x);
                             continue;
                         }
                         const int e = (int)(0xffffffffu - (uint32_t)bx);
                         const int u = p.eu[e], v = p.ev[e];
                         const uint32_t ks = p.eslot[e];
                         const int other = comp[u] == x ? comp[v] : comp[u];
-                        order[x] = (best[other] == bx && x < other) ? (int16_t)x : (int16_t)other;  // hook
+                        // hook (both roots chose this edge: the smaller id stays a root)
+                        set_tgt(x, ((uint32_t)best[other] == (uint32_t)bx && x < other) ? x : other);
                         hooked = true;
                         // record the tree edge on both endpoints (the other end's index in the row)
                         tadj_or(u, 1u << (ks & 0xffu));
@@ -272,9 +299,9 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                     FC_PROF(15, 1);
                     for (int x = lane; x < n; x += kWave) {
                         if (comp[x] != x) continue;
-                        int r = order[x];
-                        for (int r2 = order[r]; r2 != r; r2 = order[r]) r = r2;
-                        order[x] = (int16_t)r;
+                        int r = tgt(x);
+                        for (int r2 = tgt(r); r2 != r; r2 = tgt(r)) r = r2;
+                        set_tgt(x, r);
                     }
                     wave_sync();
                     for (int x0 = lane; x0 < n; x0 += kJumpU * kWave) {  // kJumpU reads in flight
@@ -282,7 +309,7 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
 #pragma unroll
                         for (int u = 0; u < kJumpU; ++u) cxs[u] = x0 + u * kWave < n ? (int)comp[x0 + u * kWave] : -1;
 #pragma unroll
-                        for (int u = 0; u < kJumpU; ++u) rts[u] = cxs[u] >= 0 ? (int)order[cxs[u]] : -1;
+                        for (int u = 0; u < kJumpU; ++u) rts[u] = cxs[u] >= 0 ? tgt(cxs[u]) : -1;
 #pragma unroll
                         for (int u = 0; u < kJumpU; ++u)
                             if (rts[u] != cxs[u]) comp[x0 + u * kWave] = (int16_t)rts[u];
