@@ -270,23 +270,41 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                     FC_STAMP(t_b1);
                     FC_PROF(3, t_b1 - t_b0);
                     bool hooked = false;
-                    for (int x = lane; x < n; x += kWave) {
-                        if (comp[x] != x) continue;
-                        const uint64_t bx = best[x];
-                        if (bx == 0) {  // no edge out (M's last component)
-                            set_tgt(x, x);
-                            continue;
+                    for (int x0 = lane; x0 < n; x0 += kJumpU * kWave) {  // kJumpU roots' reads in flight
+                        bool rt[kJumpU];
+                        uint64_t bxs[kJumpU];
+                        int es[kJumpU], us[kJumpU], vs[kJumpU];
+                        uint32_t kss[kJumpU];
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u) {
+                            const int x = x0 + u * kWave;
+                            rt[u] = x < n && comp[x] == x;
                         }
-                        const int e = (int)(0xffffffffu - (uint32_t)bx);
-                        const int u = p.eu[e], v = p.ev[e];
-                        const uint32_t ks = p.eslot[e];
-                        const int other = comp[u] == x ? comp[v] : comp[u];
-                        // hook (both roots chose this edge: the smaller id stays a root)
-                        set_tgt(x, ((uint32_t)best[other] == (uint32_t)bx && x < other) ? x : other);
-                        hooked = true;
-                        // record the tree edge on both endpoints (the other end's index in the row)
-                        tadj_or(u, 1u << (ks & 0xffu));
-                        tadj_or(v, 1u << (ks >> 8));
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u) bxs[u] = rt[u] ? best[x0 + u * kWave] : 0ull;
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u) {
+                            es[u] = bxs[u] ? (int)(0xffffffffu - (uint32_t)bxs[u]) : 0;
+                            us[u] = p.eu[es[u]];
+                            vs[u] = p.ev[es[u]];
+                            kss[u] = p.eslot[es[u]];
+                        }
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u) {
+                            if (!rt[u]) continue;
+                            const int x = x0 + u * kWave;
+                            if (bxs[u] == 0) {  // no edge out (M's last component)
+                                set_tgt(x, x);
+                                continue;
+                            }
+                            const int other = comp[us[u]] == x ? comp[vs[u]] : comp[us[u]];
+                            // hook (both roots chose this edge: the smaller id stays a root)
+                            set_tgt(x, ((uint32_t)best[other] == (uint32_t)bxs[u] && x < other) ? x : other);
+                            hooked = true;
+                            // record the tree edge on both endpoints (the other end's index in the row)
+                            tadj_or(us[u], 1u << (kss[u] & 0xffu));
+                            tadj_or(vs[u], 1u << (kss[u] >> 8));
+                        }
                     }
                     wave_sync();
                     FC_STAMP(t_b2);
@@ -297,11 +315,20 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
                     // every node takes its old root's new root -- two passes, where pointer jumping
                     // over all nodes took about four per round
                     FC_PROF(15, 1);
-                    for (int x = lane; x < n; x += kWave) {
-                        if (comp[x] != x) continue;
-                        int r = tgt(x);
-                        for (int r2 = tgt(r); r2 != r; r2 = tgt(r)) r = r2;
-                        set_tgt(x, r);
+                    for (int x0 = lane; x0 < n; x0 += kJumpU * kWave) {
+                        bool rt[kJumpU];
+                        int rs[kJumpU];
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u) rt[u] = x0 + u * kWave < n && comp[x0 + u * kWave] == x0 + u * kWave;
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u) rs[u] = rt[u] ? tgt(x0 + u * kWave) : 0;
+#pragma unroll
+                        for (int u = 0; u < kJumpU; ++u) {
+                            if (!rt[u]) continue;
+                            int r = rs[u];
+                            for (int r2 = tgt(r); r2 != r; r2 = tgt(r)) r = r2;
+                            set_tgt(x0 + u * kWave, r);
+                        }
                     }
                     wave_sync();
                     for (int x0 = lane; x0 < n; x0 += kJumpU * kWave) {  // kJumpU reads in flight
