@@ -513,9 +513,6 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
         // ---- 5. the proposed state: subtree(child) -> parts[0], rest of M -> parts[1] --------
         FC_STAMP(t_5a);
         auto na = [&](int x) -> int { return inM(x) ? (spop[x] < 0 ? d0 : d1) : a[x]; };
-        int cc = 0;
-        for (int e = lane; e < E; e += kWave) cc += na(p.eu[e]) != na(p.ev[e]);
-        const int cut_new = (int)wave_sum64(cc);
         const int64_t p1 = popM - p0;
         int flags;
         if (p0 < pop_lo || p0 > pop_hi || p1 < pop_lo || p1 > pop_hi) {
@@ -525,21 +522,37 @@ __global__ __launch_bounds__(256) void recom_kernel(RecomParams p) {
             ++steps;
             --rem;
             flags = 1;
+            // one pass over the nodes' neighbour rows: |cut'| (every cut edge seen from both
+            // ends) and |B'| (nodes with a neighbour in another district)
+            int cc = 0, bb = 0;
+            for (int x0 = lane; x0 < n; x0 += kJumpU * kWave) {
+                uint4 nw[kJumpU][RMAX / 4];
+#pragma unroll
+                for (int u = 0; u < kJumpU; ++u) {
+                    const int xc = x0 + u * kWave < n ? x0 + u * kWave : x0;
+#pragma unroll
+                    for (int q = 0; q < RMAX / 4; ++q)
+                        nw[u][q] = q < nq ? NB[(size_t)xc * nq + q] : make_uint4(~0u, ~0u, ~0u, ~0u);
+                }
+#pragma unroll
+                for (int u = 0; u < kJumpU; ++u) {
+                    if (x0 + u * kWave >= n) break;
+                    const int ax = na(x0 + u * kWave);
+                    int dn = 0;
+#pragma unroll
+                    for (int j = 0; j < RMAX; ++j) {
+                        const uint32_t y = word4(nw[u][j >> 2], j & 3) & 0xffffu;
+                        dn += (y != 0xffffu && na((int)y) != ax) ? 1 : 0;
+                    }
+                    cc += dn;
+                    bb += dn > 0 ? 1 : 0;
+                }
+            }
+            const int cut_new = (int)(wave_sum64(cc) / 2);
             // cut_accept: random() < base ** (cut - cut'), table over cut - cut' in [-E, E]
             if (mant53(w.x1, w.x2) < p.accept_thresh[cut - cut_new + E]) {
                 flags |= 2;
                 ++accepted;
-                int bb = 0;
-                for (int x = lane; x < n; x += kWave) {
-                    const NodeRec<RMAX> r = G[x];
-                    const uint32_t nbr = (uint32_t)(r.meta >> kMetaNbrShift) & 0xffffu;
-                    const int ax = na(x);
-                    int f = 0;
-#pragma unroll
-                    for (int j = 0; j < RMAX; ++j)
-                        if ((nbr >> j) & 1u) f |= na(ring_entry<RMAX>(r.ring, j)) != ax;
-                    bb += f;
-                }
                 nb = (int)wave_sum64(bb);
                 wave_sync();
                 for (int x = lane; x < n; x += kWave) a[x] = (int8_t)na(x);
